@@ -1,0 +1,277 @@
+"""Headline benchmark: ratings processed per second per ALS iteration
+(BASELINE.json metric), MovieLens-full shape, k = 64, on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--k 64]
+                    [--shape ml-full] [--solver cg|cholesky] [--no-cpu]
+
+A step is one full ALS iteration of the reference loop (user half-step:
+normal equations from gathered item rows + global block-CG solve; item
+half-step likewise with ratings minus user bias), on data resident in HBM.
+For N > 1 it runs under torch.distributed.run, one rank per GPU, users and
+items sharded by rating count (weak scaling is not available for a fixed
+data set: per-rank work shrinks as N grows -> "strong").
+
+Printed on rank 0: ONE JSON line with the contract fields plus
+``roofline`` (dominant kernel, from HIP events on the engine's stream over the
+timed region) and ``cpu_baseline`` (the reference library compiled from
+/root/reference sources, oracle/_ref/cpp_ls_lib.so, timed on a bounded
+sample of the same workload; N = 1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from movie_recommender_amd import synth  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_PEAK_TFS = 157.3        # MI355X FP32 vector / f32-MFMA dense peak
+METRIC = "ratings/sec per ALS iteration (MovieLens-full, k=64); RMSE parity"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def load_data(shape, k, cache_dir="/tmp"):
+    path = os.path.join(cache_dir, f"mr_bench_{shape}_k{k}_{synth.DATA_SEED}.npz")
+    if os.path.exists(path):
+        with np.load(path, allow_pickle=False) as d:
+            rs = synth.RatingSet(d["u"], d["i"], d["r"], int(d["nu"]), int(d["ni"]), k)
+            return rs
+    rs = synth.movielens_like(shape, k)
+    try:
+        np.savez(path, u=rs.user_ids, i=rs.item_ids, r=rs.ratings, nu=rs.num_users,
+                 ni=rs.num_items)
+    except OSError:
+        pass
+    return rs
+
+
+def algorithmic_cost(cls, k, n_users, n_items, n_ratings, ldk):
+    """(bytes, flops) per launch of a kernel class; definitions in DESIGN.md."""
+    K = k + 1
+    if cls == "matvec_users":
+        E = n_users
+        g = E * (k * ldk + ldk + 1) * 4            # G_e (S, s, n) read once
+        v = E * (ldk + 1) * 4 * 4                 # p read+write, r read, Ap write
+        return g + v, E * 2.0 * K * K
+    if cls == "matvec_items":
+        E = n_items
+        return E * k * ldk * 4 + E * ldk * 4 * 4, E * 2.0 * k * k
+    if cls == "gram_users":
+        # per rating: (idx, value) 8 B + gathered item row k*4 B; output E*K^2
+        b = n_ratings * (8 + 4 * k) + n_users * (k * ldk + 2 * ldk + 2) * 4
+        return b, n_ratings * (2.0 * K * K + 2.0 * K)
+    if cls == "gram_items":
+        b = n_ratings * (8 + 4 * (k + 1)) + n_items * (k * ldk + ldk) * 4
+        return b, n_ratings * (2.0 * k * k + 2.0 * k)
+    if cls == "cg_update":
+        E = (n_users * (ldk + 1) + n_items * ldk) / 2.0   # average side
+        return E * 6 * 4, E * 4.0
+    return 0, 0
+
+
+def cpu_baseline(rs, k, threads, frac, seed=0):
+    """Reference CPU path on a bounded sample: a random fraction of users with
+    all their ratings (ids compacted), t_iter = (T(3) - T(1)) / 2 as in
+    BASELINE.md.  Returns a dict for the JSON line, or None if unavailable."""
+    from oracle import ref
+    if not ref.available():
+        return None
+    rng = np.random.default_rng(seed)
+    keep_users = rng.random(rs.num_users) < frac
+    sel = keep_users[rs.user_ids]
+    u = rs.user_ids[sel]
+    i = rs.item_ids[sel]
+    r = rs.ratings[sel]
+    _, u = np.unique(u, return_inverse=True)
+    _, i = np.unique(i, return_inverse=True)
+    u = u.astype(np.int32)
+    i = i.astype(np.int32)
+    nu, ni = int(u.max()) + 1, int(i.max()) + 1
+    U0, V0 = ref.init_factors(nu, ni, k, 0)
+    ref.set_thread_count(threads)
+    t = {}
+    its = {}
+    for n_it in (1, 3):
+        t0 = time.perf_counter()
+        _, _, ret = ref.als(u, i, r, k, U0, V0, max_iteration=n_it)
+        t[n_it] = time.perf_counter() - t0
+        its[n_it] = ret
+    t_iter = (t[3] - t[1]) / 2.0
+    return {"value": len(r) / t_iter, "unit": "ratings/s", "cores": threads,
+            "kind": "reference",
+            "sample": (f"{frac:.3f} of users of the same workload with all their ratings: "
+                       f"N={len(r)}, users={nu}, items={ni}, k={k}; t_iter=(T(3)-T(1))/2 = "
+                       f"{t_iter:.3f} s (T1={t[1]:.2f} s, T3={t[3]:.2f} s); "
+                       f"oracle/_ref/cpp_ls_lib.so built from /root/reference/cpp/ls_lib -O2")}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--k", type=int, default=64)
+    ap.add_argument("--shape", default="ml-full")
+    ap.add_argument("--solver", default="cg", choices=["cg", "cholesky"])
+    ap.add_argument("--ridge", type=float, default=0.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-frac", type=float, default=0.08)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r01.json"),
+                    help="per-kernel HBM bytes from a rocprofv3 --pmc run (optional)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist = tdist
+
+    from movie_recommender_amd.engine import AlsContext
+    from movie_recommender_amd.distributed import TorchComm, sharded_context
+
+    t0 = time.perf_counter()
+    rs = load_data(args.shape, args.k)
+    k = args.k
+    log(f"[bench] data {args.shape} k={k}: N={rs.n} users={rs.num_users} "
+        f"items={rs.num_items} ({time.perf_counter() - t0:.1f} s)")
+    rng = np.random.RandomState(0)
+    U0 = rng.uniform(-1, 1, rs.num_users * (k + 1))
+    V0 = rng.uniform(-1, 1, rs.num_items * k)
+
+    t0 = time.perf_counter()
+    if world > 1:
+        comm = TorchComm(device=f"cuda:{local_rank}")
+        ctx = sharded_context(rs.user_ids, rs.item_ids, rs.ratings, k, rs.num_users,
+                              rs.num_items, local_rank, comm, solver=args.solver,
+                              ridge=args.ridge)
+    else:
+        ctx = AlsContext(rs.user_ids, rs.item_ids, rs.ratings, k, rs.num_users,
+                         rs.num_items, device=local_rank, solver=args.solver,
+                         ridge=args.ridge)
+    ctx.set_factors(U0, V0)
+    ctx.sync()
+    log(f"[bench] context built in {time.perf_counter() - t0:.2f} s")
+
+    for w in range(args.warmup):
+        ctx.iterate(1)
+    ctx.sync()
+    ctx.reset_stats()
+    ctx.set_timing(True)
+
+    def barrier():
+        ctx.sync()
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    t_start = time.perf_counter()
+    for s in range(args.steps):
+        ctx.iterate(1)
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    if dist is not None:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    st = ctx.stats()
+    ctx.set_timing(False)
+
+    # local work units (ratings processed by this rank per iteration)
+    n_local_users = ctx.num_ratings
+    total_ratings = rs.n
+    value = total_ratings * args.steps / elapsed
+    ms_per_step = elapsed * 1e3 / args.steps
+
+    # dominant kernel and its roofline (rank 0's kernels)
+    ldk = (k + 3) // 4 * 4
+    best = max(st["kernel_ms"].items(), key=lambda kv: kv[1])
+    cls, tot_ms = best
+    launches = max(1, st["kernel_launches"][cls])
+    avg_s = tot_ms / launches / 1e3
+    nU = rs.num_users // world if world > 1 else rs.num_users
+    nI = rs.num_items // world if world > 1 else rs.num_items
+    nbytes, nflops = algorithmic_cost(cls, k, nU, nI, n_local_users // max(1, 1), ldk)
+    bound = "mfma" if cls.startswith("gram") and k >= 32 else "hbm"
+    if bound == "hbm":
+        achieved, peak, unit = nbytes / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
+    else:
+        achieved, peak, unit = nflops / avg_s / 1e12, FP32_PEAK_TFS, "TFLOP/s"
+    traffic = None
+    if os.path.exists(args.pmc):
+        with open(args.pmc) as f:
+            pmc = json.load(f)
+        traffic = pmc.get("hbm_bytes_per_launch", {}).get(cls)
+    kernel_table = {}
+    for c, ms in st["kernel_ms"].items():
+        n = st["kernel_launches"][c]
+        if n:
+            b, fl = algorithmic_cost(c, k, nU, nI, n_local_users, ldk)
+            kernel_table[c] = {"total_ms": round(ms, 3), "launches": n,
+                               "avg_us": round(ms / n * 1e3, 2),
+                               "alg_GBps": round(b / (ms / n / 1e3) / 1e9, 1) if b else None,
+                               "alg_TFps": round(fl / (ms / n / 1e3) / 1e12, 2) if fl else None}
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "ratings/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (MovieLens-full shape, seeded; no MovieLens data offline)",
+        "config": {"workload": f"ALS iteration, {args.shape} shape, k={k}, solver={args.solver}",
+                   "k": k, "n_ratings": int(rs.n), "users": int(rs.num_users),
+                   "items": int(rs.num_items), "solver": args.solver,
+                   "parallelism": f"shard{world}" if world > 1 else "single"},
+        "roofline": {"kernel": cls, "bound": bound, "achieved": round(achieved, 2),
+                     "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
+                     "traffic": traffic,
+                     "alg_bytes_per_launch": int(nbytes), "alg_flops_per_launch": int(nflops),
+                     "avg_launch_us": round(avg_s * 1e6, 2)},
+        "cg_iterations": {"users_total": st["cg_users_total"],
+                          "items_total": st["cg_items_total"],
+                          "per_step_users": st["cg_users_total"] / args.steps,
+                          "per_step_items": st["cg_items_total"] / args.steps},
+        "kernels": kernel_table,
+        "phase_ms_per_step": {p: round(v / args.steps, 3) for p, v in st["phase_ms"].items()},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        try:
+            cb = cpu_baseline(rs, k, args.cpu_threads, args.cpu_frac)
+        except Exception as e:  # the GPU number stands on its own
+            log(f"[bench] cpu baseline failed: {e!r}")
+            cb = None
+        out["cpu_baseline"] = cb
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    ctx.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,159 @@
+/*
+ * mr_als.h -- device-resident ALS engine for MI355X (gfx950).
+ *
+ * Richer native API beside the reference ABI of cpp_ls_lib.h (SURVEY.md
+ * section 8(b), "Richer native API").  A context keeps the ratings (by-user
+ * CSR and by-item CSR), both factor tables and every solver buffer resident
+ * in HBM across iterations; only factors cross PCIe, on request.
+ *
+ * The hot path is one ALS iteration of the reference's als()
+ * (cpp/ls_lib/matrix.cpp:814-890): user half-step (normal equations from
+ * gathered item-factor rows, then the solve) and item half-step (the same with
+ * user-factor rows and ratings minus user bias).
+ *
+ * Solvers:
+ *   MR_SOLVER_CG        reference-faithful: one global conjugate-gradient run
+ *                       per half-step over the block-diagonal A^T A with the
+ *                       reference's scalars and stop rules (matrix.cpp:456-529)
+ *   MR_SOLVER_CHOLESKY  exact per-entity solve (G_e + ridge I) x_e = c_e
+ *
+ * Sharding (multi-GPU, one process per GPU): a context may own a contiguous
+ * range of users and of items (mr_als_create_shard); factor tables stay
+ * replicated, and the caller exchanges the freshly solved shard between
+ * half-steps (all-gather) and the two CG scalars per CG iteration
+ * (all-reduce) through the mr_comm callbacks.
+ */
+#ifndef MR_ALS_H
+#define MR_ALS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mr_als mr_als;
+
+enum { MR_SOLVER_CG = 0, MR_SOLVER_CHOLESKY = 1 };
+enum { MR_SIDE_USERS = 0, MR_SIDE_ITEMS = 1 };
+
+/* Kernel classes timed with HIP events when timing is enabled. */
+enum {
+  MR_K_GRAM_USERS = 0,   /* normal equations, user side (MFMA gather-Gram)   */
+  MR_K_GRAM_ITEMS,       /* normal equations, item side                       */
+  MR_K_SLAB_REDUCE,      /* combine partial normal equations of split entities */
+  MR_K_MATVEC_USERS,     /* CG batched block GEMV, user side                  */
+  MR_K_MATVEC_ITEMS,     /* CG batched block GEMV, item side                  */
+  MR_K_CG_UPDATE,        /* CG x/r update + r.r partials (both sides)         */
+  MR_K_CG_CONTROL,       /* CG scalar reduction / stop rule (both sides)      */
+  MR_K_SOLVE,            /* batched Cholesky (exact mode)                      */
+  MR_K_COUNT
+};
+
+typedef struct mr_stats {
+  int iterations;                 /* ALS iterations executed                  */
+  int last_cg_users, last_cg_items;   /* CG iterations of the last half-steps */
+  long long cg_users_total, cg_items_total;
+  double last_final_rr;           /* item-side final rr of the last iteration */
+  long long nonpd_users, nonpd_items; /* exact mode: blocks left unsolved     */
+  double kernel_ms[MR_K_COUNT];   /* summed HIP-event time per kernel class   */
+  long long kernel_launches[MR_K_COUNT]; /* timed (non-idle) launches        */
+  double phase_ms[4];             /* gram users, solve users, gram items, solve items */
+} mr_stats;
+
+/* Collective callbacks for sharded runs (one process per GPU).  The engine
+ * stages the exchanged data through pinned host memory and calls:
+ *   allreduce_f64(user, buf, count)   in-place sum over ranks of `count`
+ *                                     doubles (the CG scalars p.Ap, r.r)
+ *   allgather_rows(user, table, row_floats, row_begin, world)
+ *                                     in-place all-gather of a row table:
+ *                                     rank r owns rows [row_begin[r],
+ *                                     row_begin[r+1]) of width row_floats
+ * Both return 0 on success. */
+typedef struct mr_comm {
+  void* user;
+  int rank, world;
+  int (*allreduce_f64)(void* user, double* host_buf, int count);
+  int (*allgather_rows)(void* user, float* host_table, long long row_floats,
+                        const long long* row_begin, int world);
+} mr_comm;
+
+/* Context from host COO ratings (zero-based ids).  Builds the by-user and
+ * by-item CSR on the device.  k <= 128.  NULL on error (see mr_last_error). */
+mr_als* mr_als_create(int device, int k, int num_users, int num_items,
+                      long long n_ratings, const int* user_ids,
+                      const int* item_ids, const double* ratings);
+
+/* Sharded context: this rank solves users [u_begin,u_end) and items
+ * [i_begin,i_end).  The user view holds every rating of the rank's users,
+ * the item view every rating of its items (global ids).  Factor tables stay
+ * replicated (full U x (k+1) and I x k). */
+mr_als* mr_als_create_shard(int device, int k, int num_users, int num_items,
+                            long long n_user_view, const int* uv_user_ids,
+                            const int* uv_item_ids, const double* uv_ratings,
+                            long long n_item_view, const int* iv_user_ids,
+                            const int* iv_item_ids, const double* iv_ratings,
+                            int u_begin, int u_end, int i_begin, int i_end);
+
+/* Attach collectives: user_begin/item_begin hold world+1 shard boundaries. */
+int mr_als_set_comm(mr_als* ctx, const mr_comm* comm,
+                    const long long* user_begin, const long long* item_begin);
+
+void mr_als_destroy(mr_als* ctx);
+
+/* Factor tables in the reference layout: U[num_users*(k+1)] (row = k factors,
+ * bias), V[num_items*k]; fp64 on the host, fp32 on the device. */
+int mr_als_set_factors(mr_als* ctx, const double* U, const double* V);
+int mr_als_get_factors(mr_als* ctx, double* U, double* V);
+
+int mr_als_set_solver(mr_als* ctx, int solver, double ridge);
+/* Timing of every kernel launch with HIP events (off by default). */
+int mr_als_set_timing(mr_als* ctx, int enable);
+/* Ratings per Gram work item: heavier entities are split across waves and
+ * their partial normal equations combined in order.  Applies to contexts
+ * created afterwards (default 2048). */
+int mr_set_gram_chunk(int chunk);
+
+/* The reference loop (matrix.cpp:814-892): returns the iteration index at
+ * exit, exactly as als_from_python.  <0 on error. */
+int mr_als_run(mr_als* ctx, double min_r_decrease, int max_iteration);
+/* Exactly n ALS iterations (no outer stop test).  0 on success. */
+int mr_als_iterate(mr_als* ctx, int n);
+/* One half-step: side MR_SIDE_USERS or MR_SIDE_ITEMS.  Returns the CG
+ * iteration count (CG mode) or 0; *final_rr may be NULL. */
+int mr_als_half_step(mr_als* ctx, int side, double* final_rr);
+
+/* Build (only) the normal equations of one side from the current factors. */
+int mr_als_build_normal_equations(mr_als* ctx, int side);
+/* Copy the normal equations of n local entities of `side` (as last built):
+ * G_out[n*K*K], c_out[n*K], K = k+1 for users (bias row/column last), k for
+ * items.  For checking the Gram kernel at any problem size. */
+int mr_als_get_normal_equations(mr_als* ctx, int side, int n, const int* entities,
+                                double* G_out, double* c_out);
+
+int mr_als_get_stats(mr_als* ctx, mr_stats* out);
+int mr_als_reset_stats(mr_als* ctx);
+/* Waits for all work queued on the context's stream. */
+int mr_als_sync(mr_als* ctx);
+/* The context's HIP stream (hipStream_t) for callers that enqueue around it. */
+void* mr_als_stream(mr_als* ctx);
+
+/* Sizes/counters for reporting: N (ratings held), U, I, k. */
+long long mr_als_num_ratings(mr_als* ctx);
+
+/* Device-side pointers of the fp32 factor tables (row stride ldk floats,
+ * ldk = k rounded up to 4): Ufac[U*ldk], Ubias[U], Vfac[I*ldk]. */
+int mr_als_device_tables(mr_als* ctx, float** Ufac, float** Ubias,
+                         float** Vfac, int* ldk);
+
+/* Predictions u[:k].v + u[k] for n (user,item) pairs, on the device. */
+int mr_als_predict(mr_als* ctx, long long n, const int* user_ids,
+                   const int* item_ids, double* out);
+
+const char* mr_last_error(void);
+int mr_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MR_ALS_H */

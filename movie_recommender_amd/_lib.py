@@ -1,0 +1,146 @@
+"""ctypes binding of ``movie_recommender_amd/lib/cpp_ls_lib.so`` (gfx950 HIP).
+
+The shared library exports the reference ABI (``include/cpp_ls_lib.h``) and
+the device-resident engine API (``include/mr_als.h``).  There is no CPU
+fallback: if the library is missing or cannot load, every entry point raises.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "cpp_ls_lib.so")
+
+K_NAMES = ["gram_users", "gram_items", "slab_reduce", "matvec_users",
+           "matvec_items", "cg_update", "cg_control", "solve"]
+
+
+class MrStats(ctypes.Structure):
+    _fields_ = [("iterations", ctypes.c_int),
+                ("last_cg_users", ctypes.c_int),
+                ("last_cg_items", ctypes.c_int),
+                ("cg_users_total", ctypes.c_longlong),
+                ("cg_items_total", ctypes.c_longlong),
+                ("last_final_rr", ctypes.c_double),
+                ("nonpd_users", ctypes.c_longlong),
+                ("nonpd_items", ctypes.c_longlong),
+                ("kernel_ms", ctypes.c_double * len(K_NAMES)),
+                ("kernel_launches", ctypes.c_longlong * len(K_NAMES)),
+                ("phase_ms", ctypes.c_double * 4)]
+
+    def as_dict(self):
+        return {
+            "iterations": self.iterations,
+            "last_cg_users": self.last_cg_users,
+            "last_cg_items": self.last_cg_items,
+            "cg_users_total": self.cg_users_total,
+            "cg_items_total": self.cg_items_total,
+            "last_final_rr": self.last_final_rr,
+            "nonpd_users": self.nonpd_users,
+            "nonpd_items": self.nonpd_items,
+            "kernel_ms": {n: self.kernel_ms[i] for i, n in enumerate(K_NAMES)},
+            "kernel_launches": {n: self.kernel_launches[i] for i, n in enumerate(K_NAMES)},
+            "phase_ms": {"gram_users": self.phase_ms[0], "solve_users": self.phase_ms[1],
+                         "gram_items": self.phase_ms[2], "solve_items": self.phase_ms[3]},
+        }
+
+
+ALLREDUCE_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p,
+                                ctypes.POINTER(ctypes.c_double), ctypes.c_int)
+ALLGATHER_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p,
+                                ctypes.POINTER(ctypes.c_float), ctypes.c_longlong,
+                                ctypes.POINTER(ctypes.c_longlong), ctypes.c_int)
+
+
+class MrComm(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p),
+                ("rank", ctypes.c_int),
+                ("world", ctypes.c_int),
+                ("allreduce_f64", ALLREDUCE_CB),
+                ("allgather_rows", ALLGATHER_CB)]
+
+
+_lib = None
+
+IP = ctypes.POINTER(ctypes.c_int)
+DP = ctypes.POINTER(ctypes.c_double)
+FP = ctypes.POINTER(ctypes.c_float)
+LLP = ctypes.POINTER(ctypes.c_longlong)
+VP = ctypes.c_void_p
+
+# name -> (restype, argtypes); every symbol of include/*.h
+SIGNATURES = {
+    # reference ABI (include/cpp_ls_lib.h)
+    "set_thread_count": (None, [ctypes.c_int]),
+    "get_thread_count": (ctypes.c_int, []),
+    "cg_least_squares_from_python": (
+        ctypes.c_int, [ctypes.c_int, ctypes.c_int, IP, IP, DP, ctypes.c_int, DP,
+                       ctypes.c_int, DP, ctypes.c_double, ctypes.c_int, DP]),
+    "cg_least_squares2_from_python": (
+        ctypes.c_int, [ctypes.c_int, ctypes.c_int, IP, IP, DP, ctypes.c_int, DP,
+                       ctypes.c_int, DP, ctypes.c_double, ctypes.c_int, DP]),
+    "als_from_python": (
+        ctypes.c_int, [IP, IP, ctypes.c_int, DP, ctypes.c_int, ctypes.c_int, DP,
+                       ctypes.c_int, DP, ctypes.c_double, ctypes.c_int, ctypes.c_int]),
+    # engine API (include/mr_als.h)
+    "mr_als_create": (VP, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                           ctypes.c_longlong, IP, IP, DP]),
+    "mr_als_create_shard": (VP, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_longlong, IP, IP, DP,
+                                 ctypes.c_longlong, IP, IP, DP,
+                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "mr_als_set_comm": (ctypes.c_int, [VP, ctypes.POINTER(MrComm), LLP, LLP]),
+    "mr_als_destroy": (None, [VP]),
+    "mr_als_set_factors": (ctypes.c_int, [VP, DP, DP]),
+    "mr_als_get_factors": (ctypes.c_int, [VP, DP, DP]),
+    "mr_als_set_solver": (ctypes.c_int, [VP, ctypes.c_int, ctypes.c_double]),
+    "mr_als_set_timing": (ctypes.c_int, [VP, ctypes.c_int]),
+    "mr_set_gram_chunk": (ctypes.c_int, [ctypes.c_int]),
+    "mr_als_run": (ctypes.c_int, [VP, ctypes.c_double, ctypes.c_int]),
+    "mr_als_iterate": (ctypes.c_int, [VP, ctypes.c_int]),
+    "mr_als_half_step": (ctypes.c_int, [VP, ctypes.c_int, DP]),
+    "mr_als_build_normal_equations": (ctypes.c_int, [VP, ctypes.c_int]),
+    "mr_als_get_normal_equations": (ctypes.c_int, [VP, ctypes.c_int, ctypes.c_int, IP, DP, DP]),
+    "mr_als_get_stats": (ctypes.c_int, [VP, ctypes.POINTER(MrStats)]),
+    "mr_als_reset_stats": (ctypes.c_int, [VP]),
+    "mr_als_sync": (ctypes.c_int, [VP]),
+    "mr_als_stream": (VP, [VP]),
+    "mr_als_num_ratings": (ctypes.c_longlong, [VP]),
+    "mr_als_device_tables": (ctypes.c_int, [VP, ctypes.POINTER(FP), ctypes.POINTER(FP),
+                                            ctypes.POINTER(FP), IP]),
+    "mr_als_predict": (ctypes.c_int, [VP, ctypes.c_longlong, IP, IP, DP]),
+    "mr_last_error": (ctypes.c_char_p, []),
+    "mr_device_count": (ctypes.c_int, []),
+}
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def lib():
+    """Load the HIP library (raises if it is not built: no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryMissing(
+            f"{LIB_PATH} is not built; run `python -c 'import __graft_entry__ as g; g.build()'`"
+            " or `make -C movie_recommender_amd/csrc`")
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def last_error():
+    m = lib().mr_last_error()
+    return m.decode() if m else ""
+
+
+def check(rc, what):
+    if rc is None or (isinstance(rc, int) and rc < 0):
+        raise RuntimeError(f"{what} failed: {last_error()}")
+    return rc

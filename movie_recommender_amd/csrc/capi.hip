@@ -1,0 +1,257 @@
+// extern "C" boundary of cpp_ls_lib.so.
+//
+// (1) The reference ABI (include/cpp_ls_lib.h), replacing
+//     cpp/ls_lib/ls_linux_dll.cpp:8-103 symbol for symbol.
+// (2) The device-resident engine API (include/mr_als.h).
+// No torch types, plain pointers and sizes; failures return <0 / NULL and
+// leave a message in mr_last_error() (also printed to stderr).
+#include <cstdlib>
+#include <new>
+
+#include "../../include/cpp_ls_lib.h"
+#include "engine.h"
+
+struct mr_als {
+  mr::Engine eng;
+};
+
+namespace {
+int g_thread_count = 4;     // ls_linux_dll.cpp:6 (stored verbatim, not used on the GPU)
+int g_gram_chunk = 2048;
+
+int env_device() {
+  const char* d = getenv("MR_DEVICE");
+  return d ? atoi(d) : 0;
+}
+
+template <typename F>
+int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    mr::set_error("host out of memory");
+  } catch (...) {
+    mr::set_error("unexpected C++ exception");
+  }
+  return -1;
+}
+}  // namespace
+
+extern "C" {
+
+// ---- reference ABI ----------------------------------------------------------
+void set_thread_count(int thread_count) { g_thread_count = thread_count; }
+int get_thread_count(void) { return g_thread_count; }
+
+int cg_least_squares_from_python(int A_rows, int A_cols, int* A_row_indices,
+                                 int* A_col_indices, double* A_values,
+                                 int b_length, double* b_values, int x_length,
+                                 double* x_values, double min_r_decrease,
+                                 int max_iteration, double* final_rr) {
+  return guarded([&]() -> int {
+    MR_CHECK(b_length == A_rows, "cg_least_squares: b_length != A_rows");
+    MR_CHECK(x_length == A_cols, "cg_least_squares: x_length != A_cols");
+    return mr::cg_ls_f64(env_device(), A_rows, A_cols, A_row_indices, A_col_indices,
+                         A_values, b_values, x_values, min_r_decrease, max_iteration,
+                         final_rr);
+  });
+}
+
+int cg_least_squares2_from_python(int A_rows, int A_cols, int* A_row_indices,
+                                  int* A_col_indices, double* A_values,
+                                  int b_length, double* b_values, int x_length,
+                                  double* x_values, double min_r_decrease,
+                                  int max_iteration, double* final_rr) {
+  return cg_least_squares_from_python(A_rows, A_cols, A_row_indices, A_col_indices,
+                                      A_values, b_length, b_values, x_length, x_values,
+                                      min_r_decrease, max_iteration, final_rr);
+}
+
+int als_from_python(int* user_ids, int* item_ids, int ratings_length,
+                    double* ratings_values, int num_item_factors,
+                    int user_factors_length, double* user_factors_values,
+                    int item_factors_length, double* item_factors_values,
+                    double min_r_decrease, int max_iteration, int algorithm) {
+  (void)algorithm;
+  return guarded([&]() -> int {
+    const int k = num_item_factors;
+    MR_CHECK(k >= 1, "als: num_item_factors must be >= 1");
+    MR_CHECK(ratings_length >= 0, "als: negative ratings_length");
+    MR_CHECK(user_factors_length % (k + 1) == 0,
+             "als: user_factors_length is not a multiple of k+1");
+    MR_CHECK(item_factors_length % k == 0, "als: item_factors_length is not a multiple of k");
+    const int U = user_factors_length / (k + 1);
+    const int I = item_factors_length / k;
+    mr::Engine eng;
+    eng.chunk = g_gram_chunk;
+    if (eng.init(env_device(), k, U, I, ratings_length, user_ids, item_ids, ratings_values,
+                 ratings_length, user_ids, item_ids, ratings_values, 0, U, 0, I))
+      return -1;
+    if (eng.set_factors(user_factors_values, item_factors_values)) return -1;
+    const int ret = eng.run(min_r_decrease, max_iteration);
+    if (ret < 0) return -1;
+    if (eng.get_factors(user_factors_values, item_factors_values)) return -1;
+    return ret;
+  });
+}
+
+// ---- engine API -------------------------------------------------------------
+mr_als* mr_als_create_shard(int device, int k, int num_users, int num_items,
+                            long long n_u, const int* uv_uid, const int* uv_iid,
+                            const double* uv_r, long long n_i, const int* iv_uid,
+                            const int* iv_iid, const double* iv_r, int u_begin,
+                            int u_end, int i_begin, int i_end) {
+  mr_als* ctx = nullptr;
+  const int rc = guarded([&]() -> int {
+    ctx = new mr_als();
+    ctx->eng.chunk = g_gram_chunk;
+    return ctx->eng.init(device, k, num_users, num_items, n_u, uv_uid, uv_iid, uv_r, n_i,
+                         iv_uid, iv_iid, iv_r, u_begin, u_end, i_begin, i_end);
+  });
+  if (rc) {
+    delete ctx;
+    return nullptr;
+  }
+  return ctx;
+}
+
+mr_als* mr_als_create(int device, int k, int num_users, int num_items,
+                      long long n_ratings, const int* user_ids, const int* item_ids,
+                      const double* ratings) {
+  return mr_als_create_shard(device, k, num_users, num_items, n_ratings, user_ids,
+                             item_ids, ratings, n_ratings, user_ids, item_ids, ratings, 0,
+                             num_users, 0, num_items);
+}
+
+int mr_als_set_comm(mr_als* ctx, const mr_comm* comm, const long long* user_begin,
+                    const long long* item_begin) {
+  MR_CHECK(ctx && comm, "null argument");
+  return guarded([&]() -> int {
+    MR_CHECK(comm->world >= 1 && comm->rank >= 0 && comm->rank < comm->world, "bad comm");
+    MR_CHECK(comm->world == 1 || (comm->allreduce_f64 && comm->allgather_rows),
+             "comm callbacks missing");
+    ctx->eng.comm = *comm;
+    ctx->eng.has_comm = true;
+    ctx->eng.row_begin_u.assign(user_begin, user_begin + comm->world + 1);
+    ctx->eng.row_begin_i.assign(item_begin, item_begin + comm->world + 1);
+    return 0;
+  });
+}
+
+void mr_als_destroy(mr_als* ctx) { delete ctx; }
+
+int mr_als_set_factors(mr_als* ctx, const double* U, const double* V) {
+  MR_CHECK(ctx, "null context");
+  return guarded([&]() { return ctx->eng.set_factors(U, V); });
+}
+
+int mr_als_get_factors(mr_als* ctx, double* U, double* V) {
+  MR_CHECK(ctx, "null context");
+  return guarded([&]() { return ctx->eng.get_factors(U, V); });
+}
+
+int mr_als_set_solver(mr_als* ctx, int solver, double ridge) {
+  MR_CHECK(ctx, "null context");
+  MR_CHECK(solver == MR_SOLVER_CG || solver == MR_SOLVER_CHOLESKY, "unknown solver");
+  MR_CHECK(ridge >= 0.0, "ridge must be >= 0");
+  ctx->eng.solver = solver;
+  ctx->eng.ridge = ridge;
+  return 0;
+}
+
+int mr_als_set_timing(mr_als* ctx, int enable) {
+  MR_CHECK(ctx, "null context");
+  ctx->eng.timing = enable != 0;
+  return 0;
+}
+
+int mr_set_gram_chunk(int chunk) {
+  MR_CHECK(chunk >= 64 && chunk <= (1 << 30), "chunk must be in [64, 2^30]");
+  g_gram_chunk = chunk;
+  return 0;
+}
+
+int mr_als_run(mr_als* ctx, double min_r_decrease, int max_iteration) {
+  MR_CHECK(ctx, "null context");
+  return guarded([&]() { return ctx->eng.run(min_r_decrease, max_iteration); });
+}
+
+int mr_als_iterate(mr_als* ctx, int n) {
+  MR_CHECK(ctx, "null context");
+  return guarded([&]() { return ctx->eng.iterate(n); });
+}
+
+int mr_als_half_step(mr_als* ctx, int side, double* final_rr) {
+  MR_CHECK(ctx, "null context");
+  MR_CHECK(side == MR_SIDE_USERS || side == MR_SIDE_ITEMS, "unknown side");
+  return guarded(
+      [&]() { return ctx->eng.half_step(side == MR_SIDE_USERS, 0.01, 200, final_rr); });
+}
+
+int mr_als_build_normal_equations(mr_als* ctx, int side) {
+  MR_CHECK(ctx, "null context");
+  MR_CHECK(side == MR_SIDE_USERS || side == MR_SIDE_ITEMS, "unknown side");
+  return guarded([&]() -> int {
+    MR_HIP(hipSetDevice(ctx->eng.device));
+    if (ctx->eng.gram(side == MR_SIDE_USERS ? ctx->eng.su : ctx->eng.si)) return -1;
+    if (ctx->eng.resolve_timing(1 << 30)) return -1;
+    MR_HIP(hipStreamSynchronize(ctx->eng.stream));
+    return 0;
+  });
+}
+
+int mr_als_get_normal_equations(mr_als* ctx, int side, int n, const int* entities,
+                                double* G_out, double* c_out) {
+  MR_CHECK(ctx, "null context");
+  return guarded([&]() {
+    return ctx->eng.get_normal_equations(side == MR_SIDE_USERS, n, entities, G_out, c_out);
+  });
+}
+
+int mr_als_get_stats(mr_als* ctx, mr_stats* out) {
+  MR_CHECK(ctx && out, "null argument");
+  *out = ctx->eng.stats;
+  return 0;
+}
+
+int mr_als_reset_stats(mr_als* ctx) {
+  MR_CHECK(ctx, "null context");
+  ctx->eng.stats = mr_stats{};
+  return 0;
+}
+
+int mr_als_sync(mr_als* ctx) {
+  MR_CHECK(ctx, "null context");
+  MR_HIP(hipSetDevice(ctx->eng.device));
+  MR_HIP(hipStreamSynchronize(ctx->eng.stream));
+  return 0;
+}
+
+void* mr_als_stream(mr_als* ctx) { return ctx ? (void*)ctx->eng.stream : nullptr; }
+
+long long mr_als_num_ratings(mr_als* ctx) { return ctx ? ctx->eng.N : -1; }
+
+int mr_als_device_tables(mr_als* ctx, float** Ufac, float** Ubias, float** Vfac, int* ldk) {
+  MR_CHECK(ctx, "null context");
+  if (Ufac) *Ufac = ctx->eng.Ufac;
+  if (Ubias) *Ubias = ctx->eng.Ubias;
+  if (Vfac) *Vfac = ctx->eng.Vfac;
+  if (ldk) *ldk = ctx->eng.ldk;
+  return 0;
+}
+
+int mr_als_predict(mr_als* ctx, long long n, const int* user_ids, const int* item_ids,
+                   double* out) {
+  MR_CHECK(ctx, "null context");
+  return guarded([&]() { return ctx->eng.predict(n, user_ids, item_ids, out); });
+}
+
+const char* mr_last_error(void) { return mr::last_error(); }
+
+int mr_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+}  // extern "C"

@@ -1,0 +1,100 @@
+// Host engine state for one device-resident ALS context (see engine.hip).
+#pragma once
+#include <vector>
+
+#include "../../include/mr_als.h"
+#include "mr_internal.h"
+
+namespace mr {
+
+constexpr int kMaxParts = 2048;   // partial-sum slots (fixed grids)
+constexpr int kUpdParts = 1024;   // grid of the CG update kernels
+
+// One side of the bipartite problem: its entities' CSR rows, work list,
+// normal equations and CG vectors.  Users: K = k+1 (bias in Gs/Gn/Cb and the
+// *b vectors); items: K = k.
+struct Side {
+  bool user = false;
+  int64_t E = 0, e0 = 0, nnz = 0;
+  int64_t* off = nullptr;
+  int32_t* idx = nullptr;
+  float* val = nullptr;
+  WorkItem* work = nullptr;
+  int64_t n_work = 0;
+  SplitItem* split = nullptr;
+  int64_t n_split = 0;
+  float* slab = nullptr;
+  int64_t n_slab = 0, rec = 0;
+  float *G = nullptr, *Gs = nullptr, *Gn = nullptr, *C = nullptr, *Cb = nullptr;
+  float *r = nullptr, *p = nullptr, *q = nullptr;
+  float *rb = nullptr, *pb = nullptr, *qb = nullptr;
+  int n_part_mv = 1;
+};
+
+struct Pending {
+  int cls, tag;
+  hipEvent_t a, b;
+};
+
+struct Engine {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int k = 0, ldk = 0;
+  int64_t U = 0, I = 0, N = 0;
+  float *Ufac = nullptr, *Ubias = nullptr, *Vfac = nullptr;
+  Side su, si;
+  CgState* d_state = nullptr;
+  CgState* h_state = nullptr;
+  CgState* h_init = nullptr;
+  double* h_stage = nullptr;
+  double* partials = nullptr;
+  int* d_flag = nullptr;
+  int cur_parts = 1;
+  int solver = MR_SOLVER_CG;
+  double ridge = 0.0;
+  int chunk = 2048;
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<Pending> pending;
+  mr_stats stats{};
+  // sharded runs
+  bool has_comm = false;
+  mr_comm comm{};
+  std::vector<long long> row_begin_u, row_begin_i;
+
+  ~Engine();
+  int init(int dev, int k, int64_t U, int64_t I, int64_t n_u, const int* uv_uid,
+           const int* uv_iid, const double* uv_r, int64_t n_i, const int* iv_uid,
+           const int* iv_iid, const double* iv_r, int64_t u0, int64_t u1, int64_t i0,
+           int64_t i1);
+  int build_side(Side& S, bool user, int64_t n, const int32_t* d_key,
+                 const int32_t* d_other, const double* d_r);
+  int set_factors(const double* hU, const double* hV);
+  int get_factors(double* hU, double* hV);
+  bool sharded() const { return has_comm && comm.world > 1; }
+  int allreduce_state_slot();
+  int allgather_side(bool user);
+  int control(int phase);
+  GramDst direct_dst(Side& S);
+  GramDst slab_dst(Side& S);
+  int gram(Side& S);
+  int x_ptrs(Side& S, float** xf, float** xb);
+  int cg(Side& S, double min_dec, int max_it, double* final_rr);
+  int solve(Side& S);
+  int half_step(bool user, double min_dec, int max_it, double* final_rr);
+  int run(double min_dec, int max_it);
+  int iterate(int n);
+  int predict(int64_t n, const int* uid, const int* iid, double* out);
+  int get_normal_equations(bool user, int n, const int* ents, double* G, double* c);
+  // timing
+  int ev_get(hipEvent_t* e);
+  int tic(int cls, int tag, hipEvent_t* a);
+  int toc(int cls, int tag, hipEvent_t a);
+  int resolve_timing(int n_real);
+};
+
+int cg_ls_f64(int device, int rows, int cols, const int* rp, const int* ci,
+              const double* v, const double* b, double* x, double min_dec,
+              int max_it, double* final_rr);
+
+}  // namespace mr

@@ -1,0 +1,722 @@
+// Host-side ALS engine: device-resident context, work lists, CG driver, ALS
+// loop, sharded exchange hooks, kernel timing.
+//
+// Control flow follows the reference exactly:
+//   cg()         cg_least_squares        cpp/ls_lib/matrix.cpp:456-529
+//   run()        als() outer loop        cpp/ls_lib/matrix.cpp:814-892
+//   cg_ls_f64()  cg_least_squares on a general CSR A (ls_linux_dll.cpp:28-77)
+// but every numeric step runs on the GPU; the host only enqueues kernels and
+// reads the 72-byte CG state once per chunk of CG iterations.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "engine.h"
+
+namespace mr {
+
+// ----------------------------------------------------------------------------
+// errors
+// ----------------------------------------------------------------------------
+static thread_local std::string g_err;
+void set_error(const std::string& msg) {
+  g_err = msg;
+  if (!getenv("MR_QUIET")) fprintf(stderr, "[movie_recommender_amd] %s\n", msg.c_str());
+}
+const char* last_error() { return g_err.c_str(); }
+
+template <typename T>
+static int dalloc(T** p, int64_t n, hipStream_t s) {
+  *p = nullptr;
+  if (n <= 0) n = 1;
+  MR_HIP(hipMallocAsync((void**)p, (size_t)n * sizeof(T), s));
+  return 0;
+}
+template <typename T>
+static void dfree(T*& p, hipStream_t s) {
+  if (p) (void)hipFreeAsync(p, s);
+  p = nullptr;
+}
+
+static void free_side(Side& S, hipStream_t s) {
+  dfree(S.off, s); dfree(S.idx, s); dfree(S.val, s);
+  dfree(S.work, s); dfree(S.split, s); dfree(S.slab, s);
+  dfree(S.G, s); dfree(S.Gs, s); dfree(S.Gn, s); dfree(S.C, s); dfree(S.Cb, s);
+  dfree(S.r, s); dfree(S.p, s); dfree(S.q, s);
+  dfree(S.rb, s); dfree(S.pb, s); dfree(S.qb, s);
+}
+
+Engine::~Engine() {
+  if (stream) {
+    (void)hipSetDevice(device);
+    (void)hipStreamSynchronize(stream);
+    free_side(su, stream);
+    free_side(si, stream);
+    dfree(Ufac, stream); dfree(Ubias, stream); dfree(Vfac, stream);
+    dfree(d_state, stream); dfree(partials, stream); dfree(d_flag, stream);
+    (void)hipStreamSynchronize(stream);
+    if (h_state) (void)hipHostFree(h_state);
+    if (h_init) (void)hipHostFree(h_init);
+    if (h_stage) (void)hipHostFree(h_stage);
+    for (auto& e : ev_pool) (void)hipEventDestroy(e);
+    for (auto& p : pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
+    (void)hipStreamDestroy(stream);
+  }
+}
+
+// ----------------------------------------------------------------------------
+// timing
+// ----------------------------------------------------------------------------
+int Engine::ev_get(hipEvent_t* e) {
+  if (!ev_pool.empty()) {
+    *e = ev_pool.back();
+    ev_pool.pop_back();
+    return 0;
+  }
+  MR_HIP(hipEventCreate(e));
+  return 0;
+}
+
+int Engine::tic(int cls, int tag, hipEvent_t* a) {
+  if (!timing) return 0;
+  if (ev_get(a)) return -1;
+  MR_HIP(hipEventRecord(*a, stream));
+  (void)cls; (void)tag;
+  return 0;
+}
+
+int Engine::toc(int cls, int tag, hipEvent_t a) {
+  if (!timing) return 0;
+  hipEvent_t b;
+  if (ev_get(&b)) return -1;
+  MR_HIP(hipEventRecord(b, stream));
+  pending.push_back({cls, tag, a, b});
+  return 0;
+}
+
+// Attribute pending kernel times.  Launches tagged with a CG iteration index
+// >= n_real ran after the solve had finished (early-exit no-ops) and are not
+// counted as kernel launches.
+int Engine::resolve_timing(int n_real) {
+  if (pending.empty()) return 0;
+  MR_HIP(hipStreamSynchronize(stream));
+  for (auto& p : pending) {
+    if (p.tag < 0 || p.tag < n_real) {
+      float ms = 0.f;
+      MR_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+      stats.kernel_ms[p.cls] += ms;
+      stats.kernel_launches[p.cls] += 1;
+    }
+    ev_pool.push_back(p.a);
+    ev_pool.push_back(p.b);
+  }
+  pending.clear();
+  return 0;
+}
+
+// ----------------------------------------------------------------------------
+// construction
+// ----------------------------------------------------------------------------
+int Engine::build_side(Side& S, bool user, int64_t n, const int32_t* d_key,
+                       const int32_t* d_other, const double* d_r) {
+  S.user = user;
+  MR_CHECK(S.E >= 0, "negative entity range");
+  if (dalloc(&S.off, S.E + 1, stream) || dalloc(&S.idx, n, stream) ||
+      dalloc(&S.val, n, stream))
+    return -1;
+  S.nnz = n;
+  if (build_csr<float, double>(stream, n, S.E, d_key, (int32_t)S.e0, d_other, d_r,
+                               S.off, S.idx, S.val))
+    return -1;
+  // host copy of the offsets -> work list (chunks, heavy first)
+  std::vector<int64_t> off(S.E + 1);
+  MR_HIP(hipMemcpyAsync(off.data(), S.off, (S.E + 1) * sizeof(int64_t),
+                        hipMemcpyDeviceToHost, stream));
+  MR_HIP(hipStreamSynchronize(stream));
+  std::vector<WorkItem> work;
+  std::vector<SplitItem> split;
+  work.reserve(S.E + n / chunk + 1);
+  int32_t nslab = 0;
+  for (int64_t e = 0; e < S.E; ++e) {
+    const int64_t len = off[e + 1] - off[e];
+    if (len <= chunk) {
+      work.push_back({off[e], (int32_t)len, (int32_t)e, -1, 0});
+    } else {
+      const int32_t nc = (int32_t)((len + chunk - 1) / chunk);
+      split.push_back({(int32_t)e, nslab, nc, 0});
+      for (int32_t c = 0; c < nc; ++c) {
+        const int64_t b = off[e] + (int64_t)c * chunk;
+        const int64_t l = std::min<int64_t>(chunk, off[e + 1] - b);
+        work.push_back({b, (int32_t)l, (int32_t)e, nslab + c, 0});
+      }
+      nslab += nc;
+    }
+  }
+  std::stable_sort(work.begin(), work.end(),
+                   [](const WorkItem& a, const WorkItem& b) { return a.len > b.len; });
+  S.n_work = (int64_t)work.size();
+  S.n_split = (int64_t)split.size();
+  S.n_slab = nslab;
+  S.rec = (int64_t)k * ldk + 2 * ldk + 4;
+  if (dalloc(&S.work, S.n_work, stream) || dalloc(&S.split, S.n_split, stream) ||
+      dalloc(&S.slab, S.n_slab * S.rec, stream))
+    return -1;
+  if (S.n_work)
+    MR_HIP(hipMemcpyAsync(S.work, work.data(), S.n_work * sizeof(WorkItem),
+                          hipMemcpyHostToDevice, stream));
+  if (S.n_split)
+    MR_HIP(hipMemcpyAsync(S.split, split.data(), S.n_split * sizeof(SplitItem),
+                          hipMemcpyHostToDevice, stream));
+  // normal equations + CG vectors
+  const int64_t ef = S.E * ldk;
+  if (dalloc(&S.G, S.E * (int64_t)k * ldk, stream) || dalloc(&S.C, ef, stream) ||
+      dalloc(&S.r, ef, stream) || dalloc(&S.p, ef, stream) || dalloc(&S.q, ef, stream))
+    return -1;
+  if (user) {
+    if (dalloc(&S.Gs, ef, stream) || dalloc(&S.Gn, S.E, stream) ||
+        dalloc(&S.Cb, S.E, stream) || dalloc(&S.rb, S.E, stream) ||
+        dalloc(&S.pb, S.E, stream) || dalloc(&S.qb, S.E, stream))
+      return -1;
+  }
+  MR_HIP(hipMemsetAsync(S.r, 0, ef * sizeof(float), stream));
+  MR_HIP(hipMemsetAsync(S.p, 0, ef * sizeof(float), stream));
+  MR_HIP(hipMemsetAsync(S.q, 0, ef * sizeof(float), stream));
+  // matvec grid: one wave per entity, fixed grid for reproducible partials
+  int64_t g = (S.E + 3) / 4;
+  S.n_part_mv = (int)std::max<int64_t>(1, std::min<int64_t>(g, kMaxParts));
+  MR_HIP(hipStreamSynchronize(stream));
+  return 0;
+}
+
+int Engine::init(int dev, int k_, int64_t U_, int64_t I_, int64_t n_u,
+                 const int* uv_uid, const int* uv_iid, const double* uv_r,
+                 int64_t n_i, const int* iv_uid, const int* iv_iid,
+                 const double* iv_r, int64_t u0, int64_t u1, int64_t i0,
+                 int64_t i1) {
+  device = dev;
+  k = k_;
+  ldk = ldk_of(k);
+  U = U_;
+  I = I_;
+  MR_CHECK(k >= 1 && k <= kMaxK, "k must be in [1, 128]");
+  MR_CHECK(U >= 0 && I >= 0, "negative table size");
+  MR_CHECK(0 <= u0 && u0 <= u1 && u1 <= U && 0 <= i0 && i0 <= i1 && i1 <= I,
+           "bad shard range");
+  MR_HIP(hipSetDevice(device));
+  MR_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  MR_HIP(hipHostMalloc((void**)&h_state, sizeof(CgState), hipHostMallocDefault));
+  MR_HIP(hipHostMalloc((void**)&h_init, sizeof(CgState), hipHostMallocDefault));
+  MR_HIP(hipHostMalloc((void**)&h_stage, 64, hipHostMallocDefault));
+  if (dalloc(&d_state, 1, stream) || dalloc(&partials, kMaxParts, stream) ||
+      dalloc(&d_flag, 4, stream))
+    return -1;
+  su.e0 = u0; su.E = u1 - u0;
+  si.e0 = i0; si.E = i1 - i0;
+  // factor tables (replicated), zero padding columns
+  if (dalloc(&Ufac, U * ldk, stream) || dalloc(&Ubias, U, stream) ||
+      dalloc(&Vfac, I * ldk, stream))
+    return -1;
+  MR_HIP(hipMemsetAsync(Ufac, 0, std::max<int64_t>(1, U * ldk) * 4, stream));
+  MR_HIP(hipMemsetAsync(Ubias, 0, std::max<int64_t>(1, U) * 4, stream));
+  MR_HIP(hipMemsetAsync(Vfac, 0, std::max<int64_t>(1, I * ldk) * 4, stream));
+  // upload + build both views
+  const bool same = (uv_uid == iv_uid && uv_iid == iv_iid && uv_r == iv_r && n_u == n_i);
+  for (int view = 0; view < (same ? 1 : 2); ++view) {
+    const int64_t n = view == 0 ? n_u : n_i;
+    const int* hu = view == 0 ? uv_uid : iv_uid;
+    const int* hi = view == 0 ? uv_iid : iv_iid;
+    const double* hr = view == 0 ? uv_r : iv_r;
+    int32_t *du = nullptr, *di = nullptr;
+    double* dr = nullptr;
+    if (dalloc(&du, n, stream) || dalloc(&di, n, stream) || dalloc(&dr, n, stream)) return -1;
+    if (n > 0) {
+      MR_HIP(hipMemcpyAsync(du, hu, n * 4, hipMemcpyHostToDevice, stream));
+      MR_HIP(hipMemcpyAsync(di, hi, n * 4, hipMemcpyHostToDevice, stream));
+      MR_HIP(hipMemcpyAsync(dr, hr, n * 8, hipMemcpyHostToDevice, stream));
+    }
+    // id range validation (the reference has none: out-of-range ids are UB)
+    MR_HIP(hipMemsetAsync(d_flag, 0, 16, stream));
+    if (launch_validate_ids(stream, n, du, view == 0 || same ? (int32_t)u0 : 0,
+                            view == 0 || same ? (int32_t)u1 : (int32_t)U, d_flag))
+      return -1;
+    if (launch_validate_ids(stream, n, di, view == 1 || same ? (int32_t)i0 : 0,
+                            view == 1 || same ? (int32_t)i1 : (int32_t)I, d_flag + 1))
+      return -1;
+    int flags[2] = {0, 0};
+    MR_HIP(hipMemcpyAsync(flags, d_flag, 8, hipMemcpyDeviceToHost, stream));
+    MR_HIP(hipStreamSynchronize(stream));
+    if (view == 0 && !same) {
+      MR_CHECK(!flags[0], "user view: user id outside this shard's user range");
+      MR_CHECK(!flags[1], "user view: item id outside [0, num_items)");
+    } else if (view == 1) {
+      MR_CHECK(!flags[0], "item view: user id outside [0, num_users)");
+      MR_CHECK(!flags[1], "item view: item id outside this shard's item range");
+    } else {
+      MR_CHECK(!flags[0], "user id outside [0, num_users)");
+      MR_CHECK(!flags[1], "item id outside [0, num_items)");
+    }
+    int rc = 0;
+    if (view == 0) rc = build_side(su, true, n, du, di, dr);
+    if (rc == 0 && (view == 1 || same)) rc = build_side(si, false, n, di, du, dr);
+    dfree(du, stream); dfree(di, stream); dfree(dr, stream);
+    if (rc) return -1;
+  }
+  N = su.nnz;
+  MR_HIP(hipStreamSynchronize(stream));
+  return 0;
+}
+
+// ----------------------------------------------------------------------------
+// factors
+// ----------------------------------------------------------------------------
+int Engine::set_factors(const double* hU, const double* hV) {
+  MR_HIP(hipSetDevice(device));
+  double* tmp = nullptr;
+  const int64_t nmax = std::max(U * (k + 1), I * (int64_t)k);
+  if (dalloc(&tmp, nmax, stream)) return -1;
+  int rc = 0;
+  if (hU && U) {
+    MR_HIP(hipMemcpyAsync(tmp, hU, U * (k + 1) * 8, hipMemcpyHostToDevice, stream));
+    rc |= launch_unpack_factors(stream, U, k + 1, k, ldk, tmp, Ufac, Ubias);
+  }
+  if (hV && I) {
+    MR_HIP(hipMemcpyAsync(tmp, hV, I * (int64_t)k * 8, hipMemcpyHostToDevice, stream));
+    rc |= launch_unpack_factors(stream, I, k, k, ldk, tmp, Vfac, nullptr);
+  }
+  MR_HIP(hipStreamSynchronize(stream));
+  dfree(tmp, stream);
+  return rc ? -1 : 0;
+}
+
+int Engine::get_factors(double* hU, double* hV) {
+  MR_HIP(hipSetDevice(device));
+  double* tmp = nullptr;
+  const int64_t nmax = std::max(U * (k + 1), I * (int64_t)k);
+  if (dalloc(&tmp, nmax, stream)) return -1;
+  int rc = 0;
+  if (hU && U) {
+    rc |= launch_pack_factors(stream, U, k + 1, k, ldk, Ufac, Ubias, tmp);
+    MR_HIP(hipMemcpyAsync(hU, tmp, U * (k + 1) * 8, hipMemcpyDeviceToHost, stream));
+    MR_HIP(hipStreamSynchronize(stream));
+  }
+  if (hV && I) {
+    rc |= launch_pack_factors(stream, I, k, k, ldk, Vfac, nullptr, tmp);
+    MR_HIP(hipMemcpyAsync(hV, tmp, I * (int64_t)k * 8, hipMemcpyDeviceToHost, stream));
+    MR_HIP(hipStreamSynchronize(stream));
+  }
+  dfree(tmp, stream);
+  MR_HIP(hipStreamSynchronize(stream));
+  return rc ? -1 : 0;
+}
+
+// ----------------------------------------------------------------------------
+// collectives (sharded runs); host-staged callbacks
+// ----------------------------------------------------------------------------
+int Engine::allreduce_state_slot() {
+  if (!sharded()) return 0;
+  MR_HIP(hipMemcpyAsync(h_stage, &d_state->comm[0], sizeof(double),
+                        hipMemcpyDeviceToHost, stream));
+  MR_HIP(hipStreamSynchronize(stream));
+  MR_CHECK(comm.allreduce_f64(comm.user, (double*)h_stage, 1) == 0,
+           "allreduce callback failed");
+  MR_HIP(hipMemcpyAsync(&d_state->comm[0], h_stage, sizeof(double),
+                        hipMemcpyHostToDevice, stream));
+  return 0;
+}
+
+int Engine::allgather_side(bool user) {
+  if (!sharded()) return 0;
+  const int64_t rows = user ? U : I;
+  // gather [fac | bias] rows through host staging
+  const int64_t rowf = user ? ldk + 1 : ldk;
+  std::vector<float> tab(rows * rowf);
+  std::vector<float> fac(rows * ldk), bias(user ? rows : 0);
+  MR_HIP(hipMemcpyAsync(fac.data(), user ? Ufac : Vfac, rows * ldk * 4,
+                        hipMemcpyDeviceToHost, stream));
+  if (user)
+    MR_HIP(hipMemcpyAsync(bias.data(), Ubias, rows * 4, hipMemcpyDeviceToHost, stream));
+  MR_HIP(hipStreamSynchronize(stream));
+  for (int64_t r = 0; r < rows; ++r) {
+    memcpy(&tab[r * rowf], &fac[r * ldk], ldk * 4);
+    if (user) tab[r * rowf + ldk] = bias[r];
+  }
+  const std::vector<long long>& rb = user ? row_begin_u : row_begin_i;
+  MR_CHECK(comm.allgather_rows(comm.user, tab.data(), rowf, rb.data(), comm.world) == 0,
+           "allgather callback failed");
+  for (int64_t r = 0; r < rows; ++r) {
+    memcpy(&fac[r * ldk], &tab[r * rowf], ldk * 4);
+    if (user) bias[r] = tab[r * rowf + ldk];
+  }
+  MR_HIP(hipMemcpyAsync(user ? Ufac : Vfac, fac.data(), rows * ldk * 4,
+                        hipMemcpyHostToDevice, stream));
+  if (user)
+    MR_HIP(hipMemcpyAsync(Ubias, bias.data(), rows * 4, hipMemcpyHostToDevice, stream));
+  MR_HIP(hipStreamSynchronize(stream));
+  return 0;
+}
+
+int Engine::control(int phase) {
+  hipEvent_t a = nullptr;
+  if (tic(MR_K_CG_CONTROL, -1, &a)) return -1;
+  if (!sharded()) {
+    if (launch_cg_control(stream, d_state, phase, CTL_BOTH, partials, cur_parts)) return -1;
+  } else {
+    if (launch_cg_control(stream, d_state, phase, CTL_REDUCE, partials, cur_parts)) return -1;
+    if (allreduce_state_slot()) return -1;
+    if (launch_cg_control(stream, d_state, phase, CTL_FINALIZE, partials, cur_parts)) return -1;
+  }
+  return toc(MR_K_CG_CONTROL, -1, a);
+}
+
+// ----------------------------------------------------------------------------
+// half-step pieces
+// ----------------------------------------------------------------------------
+GramDst Engine::direct_dst(Side& S) {
+  GramDst d;
+  d.G = S.G; d.Gs = S.Gs; d.C = S.C; d.Cb = S.Cb; d.Gn = S.Gn;
+  d.sG = (int64_t)k * ldk; d.sV = ldk; d.sS = 1;
+  return d;
+}
+
+GramDst Engine::slab_dst(Side& S) {
+  GramDst d;
+  const int64_t nG = (int64_t)k * ldk;
+  d.G = S.slab; d.Gs = S.slab + nG; d.C = S.slab + nG + ldk;
+  d.Cb = S.slab + nG + 2 * ldk; d.Gn = S.slab + nG + 2 * ldk + 1;
+  d.sG = d.sV = d.sS = S.rec;
+  return d;
+}
+
+int Engine::gram(Side& S) {
+  const bool user = S.user;
+  const float* F = user ? Vfac : Ufac;
+  const float* bias = user ? nullptr : Ubias;
+  hipEvent_t a = nullptr;
+  const int cls = user ? MR_K_GRAM_USERS : MR_K_GRAM_ITEMS;
+  if (tic(cls, -1, &a)) return -1;
+  if (launch_gram(stream, user, k, S.work, S.n_work, S.idx, S.val, F, bias,
+                  direct_dst(S), slab_dst(S)))
+    return -1;
+  if (toc(cls, -1, a)) return -1;
+  if (S.n_split) {
+    if (tic(MR_K_SLAB_REDUCE, -1, &a)) return -1;
+    if (launch_slab_reduce(stream, user, k, S.split, S.n_split, S.slab, S.rec, direct_dst(S)))
+      return -1;
+    if (toc(MR_K_SLAB_REDUCE, -1, a)) return -1;
+  }
+  return 0;
+}
+
+int Engine::x_ptrs(Side& S, float** xf, float** xb) {
+  if (S.user) {
+    *xf = Ufac + S.e0 * ldk;
+    *xb = Ubias + S.e0;
+  } else {
+    *xf = Vfac + S.e0 * ldk;
+    *xb = nullptr;
+  }
+  return 0;
+}
+
+int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr) {
+  float *xf, *xb;
+  x_ptrs(S, &xf, &xb);
+  const bool user = S.user;
+  const int mv_cls = user ? MR_K_MATVEC_USERS : MR_K_MATVEC_ITEMS;
+  const int64_t n = S.E * ldk;
+  const int64_t nb = user ? S.E : 0;
+  memset(h_init, 0, sizeof(CgState));
+  h_init->min_dec = min_dec;
+  h_init->max_it = max_it;
+  MR_HIP(hipMemcpyAsync(d_state, h_init, sizeof(CgState), hipMemcpyHostToDevice, stream));
+  // r0 = G x - c ; p0 = -r0 ; rr  (matrix.cpp:464-485)
+  hipEvent_t a = nullptr;
+  if (tic(mv_cls, -1, &a)) return -1;
+  if (launch_cg_matvec(stream, user, d_state, 0, S.E, k, S.G, S.Gs, S.Gn, xf, xb,
+                       S.r, S.rb, S.q, S.qb, partials, S.n_part_mv))
+    return -1;
+  if (toc(mv_cls, -1, a)) return -1;
+  if (tic(MR_K_CG_UPDATE, -1, &a)) return -1;
+  if (launch_cg_update(stream, d_state, UPD_INIT, n, nb, xf, S.r, S.p, S.q, S.C, xb,
+                       S.rb, S.pb, S.qb, S.Cb, partials, kUpdParts))
+    return -1;
+  if (toc(MR_K_CG_UPDATE, -1, a)) return -1;
+  cur_parts = kUpdParts;
+  if (control(CG_INIT)) return -1;
+  int t = 0;
+  int chunk_it = 4;
+  while (true) {
+    for (int c = 0; c < chunk_it; ++c, ++t) {
+      if (tic(mv_cls, t, &a)) return -1;
+      if (launch_cg_matvec(stream, user, d_state, t > 0, S.E, k, S.G, S.Gs, S.Gn, S.p,
+                           S.pb, S.r, S.rb, S.q, S.qb, partials, S.n_part_mv))
+        return -1;
+      if (toc(mv_cls, t, a)) return -1;
+      cur_parts = S.n_part_mv;
+      if (control(CG_ALPHA)) return -1;
+      if (tic(MR_K_CG_UPDATE, t, &a)) return -1;
+      if (launch_cg_update(stream, d_state, UPD_STEP, n, nb, xf, S.r, S.p, S.q, S.C, xb,
+                           S.rb, S.pb, S.qb, S.Cb, partials, kUpdParts))
+        return -1;
+      if (toc(MR_K_CG_UPDATE, t, a)) return -1;
+      cur_parts = kUpdParts;
+      if (control(CG_BETA)) return -1;
+    }
+    MR_HIP(hipMemcpyAsync(h_state, d_state, sizeof(CgState), hipMemcpyDeviceToHost, stream));
+    MR_HIP(hipStreamSynchronize(stream));
+    if (h_state->done) break;
+    MR_CHECK(t <= max_it + 64, "CG did not terminate");
+    chunk_it = std::min(chunk_it * 2, 16);
+  }
+  if (resolve_timing(h_state->n_matvec)) return -1;
+  if (final_rr) *final_rr = h_state->final_rr;
+  return h_state->ret;
+}
+
+int Engine::solve(Side& S) {
+  float *xf, *xb;
+  x_ptrs(S, &xf, &xb);
+  MR_HIP(hipMemsetAsync(d_flag, 0, 4, stream));
+  hipEvent_t a = nullptr;
+  if (tic(MR_K_SOLVE, -1, &a)) return -1;
+  if (launch_solve(stream, S.user, S.E, k, ridge, S.G, S.Gs, S.Gn, S.C, S.Cb, xf, xb,
+                   d_flag))
+    return -1;
+  if (toc(MR_K_SOLVE, -1, a)) return -1;
+  int bad = 0;
+  MR_HIP(hipMemcpyAsync(&bad, d_flag, 4, hipMemcpyDeviceToHost, stream));
+  MR_HIP(hipStreamSynchronize(stream));
+  if (S.user) stats.nonpd_users += bad;
+  else stats.nonpd_items += bad;
+  return 0;
+}
+
+int Engine::half_step(bool user, double min_dec, int max_it, double* final_rr) {
+  MR_HIP(hipSetDevice(device));
+  Side& S = user ? su : si;
+  hipEvent_t p0 = nullptr, p1 = nullptr, p2 = nullptr;
+  if (timing) {
+    if (ev_get(&p0) || ev_get(&p1) || ev_get(&p2)) return -1;
+    MR_HIP(hipEventRecord(p0, stream));
+  }
+  if (gram(S)) return -1;
+  if (timing) MR_HIP(hipEventRecord(p1, stream));
+  int its = 0;
+  double rr = 0.0;
+  if (solver == MR_SOLVER_CG) {
+    its = cg(S, min_dec, max_it, &rr);
+    if (its < 0) return -1;
+  } else {
+    if (solve(S)) return -1;
+  }
+  if (allgather_side(user)) return -1;
+  if (timing) {
+    MR_HIP(hipEventRecord(p2, stream));
+    MR_HIP(hipStreamSynchronize(stream));
+    float g = 0.f, s = 0.f;
+    MR_HIP(hipEventElapsedTime(&g, p0, p1));
+    MR_HIP(hipEventElapsedTime(&s, p1, p2));
+    stats.phase_ms[user ? 0 : 2] += g;
+    stats.phase_ms[user ? 1 : 3] += s;
+    ev_pool.push_back(p0); ev_pool.push_back(p1); ev_pool.push_back(p2);
+    if (resolve_timing(1 << 30)) return -1;
+  }
+  if (user) {
+    stats.last_cg_users = its;
+    stats.cg_users_total += its;
+  } else {
+    stats.last_cg_items = its;
+    stats.cg_items_total += its;
+    stats.last_final_rr = rr;
+  }
+  if (final_rr) *final_rr = rr;
+  return its;
+}
+
+// The reference outer loop (matrix.cpp:810-892).  The user half-step uses
+// cg_least_squares' defaults (0.01, 200) as at :818; the item half-step passes
+// (0.01, 200, &rr) as at :854; min_r_decrease only drives the outer test.
+int Engine::run(double min_dec, int max_it) {
+  int it = 0;
+  double old_rr = 0.0;
+  while (it < max_it) {
+    if (half_step(true, 0.01, 200, nullptr) < 0) return -1;
+    double rr = 0.0;
+    if (half_step(false, 0.01, 200, &rr) < 0) return -1;
+    stats.iterations += 1;
+    if (it >= 3) {
+      const double decrease = (old_rr - rr) / old_rr;
+      if (decrease < min_dec) return it;
+    }
+    old_rr = rr;
+    ++it;
+  }
+  return it;
+}
+
+int Engine::iterate(int n) {
+  for (int i = 0; i < n; ++i) {
+    if (half_step(true, 0.01, 200, nullptr) < 0) return -1;
+    if (half_step(false, 0.01, 200, nullptr) < 0) return -1;
+    stats.iterations += 1;
+  }
+  return 0;
+}
+
+int Engine::predict(int64_t n, const int* uid, const int* iid, double* out) {
+  MR_HIP(hipSetDevice(device));
+  int *du = nullptr, *di = nullptr;
+  double* dout = nullptr;
+  if (dalloc(&du, n, stream) || dalloc(&di, n, stream) || dalloc(&dout, n, stream)) return -1;
+  if (n > 0) {
+    MR_HIP(hipMemcpyAsync(du, uid, n * 4, hipMemcpyHostToDevice, stream));
+    MR_HIP(hipMemcpyAsync(di, iid, n * 4, hipMemcpyHostToDevice, stream));
+    MR_HIP(hipMemsetAsync(d_flag, 0, 8, stream));
+    if (launch_validate_ids(stream, n, du, 0, (int32_t)U, d_flag)) return -1;
+    if (launch_validate_ids(stream, n, di, 0, (int32_t)I, d_flag + 1)) return -1;
+    int flags[2];
+    MR_HIP(hipMemcpyAsync(flags, d_flag, 8, hipMemcpyDeviceToHost, stream));
+    MR_HIP(hipStreamSynchronize(stream));
+    MR_CHECK(!flags[0] && !flags[1], "predict: id out of range");
+    if (launch_predict(stream, n, k, ldk, du, di, Ufac, Ubias, Vfac, dout)) return -1;
+    MR_HIP(hipMemcpyAsync(out, dout, n * 8, hipMemcpyDeviceToHost, stream));
+  }
+  MR_HIP(hipStreamSynchronize(stream));
+  dfree(du, stream); dfree(di, stream); dfree(dout, stream);
+  return 0;
+}
+
+int Engine::get_normal_equations(bool user, int n, const int* ents, double* G, double* c) {
+  MR_HIP(hipSetDevice(device));
+  Side& S = user ? su : si;
+  const int K = user ? k + 1 : k;
+  std::vector<float> g((size_t)k * ldk), v(ldk), s(ldk);
+  float cb = 0.f, gn = 0.f;
+  for (int t = 0; t < n; ++t) {
+    const int64_t e = ents[t];
+    MR_CHECK(e >= 0 && e < S.E, "entity out of range");
+    MR_HIP(hipMemcpyAsync(g.data(), S.G + e * k * ldk, (size_t)k * ldk * 4,
+                          hipMemcpyDeviceToHost, stream));
+    MR_HIP(hipMemcpyAsync(v.data(), S.C + e * ldk, ldk * 4, hipMemcpyDeviceToHost, stream));
+    if (user) {
+      MR_HIP(hipMemcpyAsync(s.data(), S.Gs + e * ldk, ldk * 4, hipMemcpyDeviceToHost, stream));
+      MR_HIP(hipMemcpyAsync(&cb, S.Cb + e, 4, hipMemcpyDeviceToHost, stream));
+      MR_HIP(hipMemcpyAsync(&gn, S.Gn + e, 4, hipMemcpyDeviceToHost, stream));
+    }
+    MR_HIP(hipStreamSynchronize(stream));
+    double* Ge = G + (size_t)t * K * K;
+    double* ce = c + (size_t)t * K;
+    for (int i = 0; i < K; ++i) {
+      for (int j = 0; j < K; ++j) {
+        double val;
+        if (i < k && j < k) val = g[(size_t)i * ldk + j];
+        else if (i < k) val = s[i];
+        else if (j < k) val = s[j];
+        else val = gn;
+        Ge[i * K + j] = val;
+      }
+      ce[i] = i < k ? v[i] : cb;
+    }
+  }
+  return 0;
+}
+
+// ----------------------------------------------------------------------------
+// General CSR CG least squares in fp64 (cg_least_squares[2]_from_python)
+// ----------------------------------------------------------------------------
+int cg_ls_f64(int device, int rows, int cols, const int* rp, const int* ci,
+              const double* v, const double* b, double* x, double min_dec,
+              int max_it, double* final_rr) {
+  MR_CHECK(rows >= 0 && cols >= 0, "negative matrix dimension");
+  MR_CHECK(rp[0] == 0 && rp[rows] >= 0, "row indices must start at 0");
+  for (int r = 0; r < rows; ++r) MR_CHECK(rp[r + 1] >= rp[r], "row indices not monotone");
+  const int64_t nnz = rp[rows];
+  for (int64_t j = 0; j < nnz; ++j)
+    MR_CHECK(ci[j] >= 0 && ci[j] < cols, "column index out of range");
+  MR_HIP(hipSetDevice(device));
+  hipStream_t s;
+  MR_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  struct Bufs {
+    hipStream_t s;
+    std::vector<void*> p;
+    ~Bufs() {
+      for (void* q : p) (void)hipFreeAsync(q, s);
+      (void)hipStreamSynchronize(s);
+      (void)hipStreamDestroy(s);
+    }
+  } bufs{s, {}};
+  auto alloc = [&](void** q, size_t bytes) -> int {
+    MR_HIP(hipMallocAsync(q, bytes ? bytes : 8, s));
+    bufs.p.push_back(*q);
+    return 0;
+  };
+  int32_t *d_rp32, *d_ci, *d_rowof, *d_tidx;
+  int64_t *d_rp, *d_toff;
+  double *d_v, *d_tval, *d_b, *d_b2, *d_x, *d_r, *d_p, *d_q, *d_t, *d_part;
+  CgState *d_st, *h_st;
+  if (alloc((void**)&d_rp32, (rows + 1) * 4) || alloc((void**)&d_rp, (rows + 1) * 8) ||
+      alloc((void**)&d_ci, nnz * 4) || alloc((void**)&d_v, nnz * 8) ||
+      alloc((void**)&d_rowof, nnz * 4) || alloc((void**)&d_toff, ((int64_t)cols + 1) * 8) ||
+      alloc((void**)&d_tidx, nnz * 4) || alloc((void**)&d_tval, nnz * 8) ||
+      alloc((void**)&d_b, (int64_t)rows * 8) || alloc((void**)&d_b2, (int64_t)cols * 8) ||
+      alloc((void**)&d_x, (int64_t)cols * 8) || alloc((void**)&d_r, (int64_t)cols * 8) ||
+      alloc((void**)&d_p, (int64_t)cols * 8) || alloc((void**)&d_q, (int64_t)cols * 8) ||
+      alloc((void**)&d_t, (int64_t)rows * 8) || alloc((void**)&d_part, kUpdParts * 8) ||
+      alloc((void**)&d_st, sizeof(CgState)))
+    return -1;
+  MR_HIP(hipHostMalloc((void**)&h_st, sizeof(CgState), hipHostMallocDefault));
+  struct HFree { CgState* h; ~HFree() { (void)hipHostFree(h); } } hf{h_st};
+  MR_HIP(hipMemcpyAsync(d_rp32, rp, (rows + 1) * 4, hipMemcpyHostToDevice, s));
+  if (nnz) {
+    MR_HIP(hipMemcpyAsync(d_ci, ci, nnz * 4, hipMemcpyHostToDevice, s));
+    MR_HIP(hipMemcpyAsync(d_v, v, nnz * 8, hipMemcpyHostToDevice, s));
+  }
+  if (rows) MR_HIP(hipMemcpyAsync(d_b, b, (int64_t)rows * 8, hipMemcpyHostToDevice, s));
+  if (cols) MR_HIP(hipMemcpyAsync(d_x, x, (int64_t)cols * 8, hipMemcpyHostToDevice, s));
+  if (launch_i32_to_i64(s, rows + 1, d_rp32, d_rp)) return -1;
+  // explicit transpose on the device (sparse_matrix_transpose, matrix.cpp:617-692)
+  if (launch_rows_of(s, rows, d_rp, d_rowof)) return -1;
+  if (build_csr<double, double>(s, nnz, cols, d_ci, 0, d_rowof, d_v, d_toff, d_tidx, d_tval))
+    return -1;
+  // b2 = A^T b
+  if (launch_spmv_f64(s, cols, d_toff, d_tidx, d_tval, d_b, d_b2)) return -1;
+  memset(h_st, 0, sizeof(CgState));
+  h_st->min_dec = min_dec;
+  h_st->max_it = max_it;
+  MR_HIP(hipMemcpyAsync(d_st, h_st, sizeof(CgState), hipMemcpyHostToDevice, s));
+  // r0 = A^T A x - b2, p0 = -r0
+  if (launch_spmv_f64(s, rows, d_rp, d_ci, d_v, d_x, d_t)) return -1;
+  if (launch_spmv_f64(s, cols, d_toff, d_tidx, d_tval, d_t, d_q)) return -1;
+  if (launch_update_f64(s, d_st, UPD_INIT, cols, d_x, d_r, d_p, d_q, d_b2, d_part, kUpdParts))
+    return -1;
+  if (launch_cg_control(s, d_st, CG_INIT, CTL_BOTH, d_part, kUpdParts)) return -1;
+  int t = 0, chunk_it = 4;
+  while (true) {
+    for (int c = 0; c < chunk_it; ++c, ++t) {
+      if (t > 0 && launch_p_update_f64(s, d_st, cols, d_p, d_r)) return -1;
+      if (launch_spmv_f64(s, rows, d_rp, d_ci, d_v, d_p, d_t)) return -1;
+      if (launch_spmv_f64(s, cols, d_toff, d_tidx, d_tval, d_t, d_q)) return -1;
+      if (launch_dot_f64(s, d_st, cols, d_p, d_q, d_part, kUpdParts)) return -1;
+      if (launch_cg_control(s, d_st, CG_ALPHA, CTL_BOTH, d_part, kUpdParts)) return -1;
+      if (launch_update_f64(s, d_st, UPD_STEP, cols, d_x, d_r, d_p, d_q, d_b2, d_part,
+                            kUpdParts))
+        return -1;
+      if (launch_cg_control(s, d_st, CG_BETA, CTL_BOTH, d_part, kUpdParts)) return -1;
+    }
+    MR_HIP(hipMemcpyAsync(h_st, d_st, sizeof(CgState), hipMemcpyDeviceToHost, s));
+    MR_HIP(hipStreamSynchronize(s));
+    if (h_st->done) break;
+    MR_CHECK(t <= max_it + 64, "CG did not terminate");
+    chunk_it = std::min(chunk_it * 2, 16);
+  }
+  if (cols) MR_HIP(hipMemcpyAsync(x, d_x, (int64_t)cols * 8, hipMemcpyDeviceToHost, s));
+  MR_HIP(hipStreamSynchronize(s));
+  if (final_rr) *final_rr = h_st->final_rr;
+  return h_st->ret;
+}
+
+}  // namespace mr

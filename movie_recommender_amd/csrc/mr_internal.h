@@ -1,0 +1,141 @@
+// Internal declarations shared by the HIP kernels and the host engine.
+// Target: MI355X (gfx950, CDNA4) only.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+namespace mr {
+
+// Error handling --------------------------------------------------------------
+void set_error(const std::string& msg);
+const char* last_error();
+
+#define MR_HIP(call)                                                          \
+  do {                                                                        \
+    hipError_t _e = (call);                                                   \
+    if (_e != hipSuccess) {                                                   \
+      ::mr::set_error(std::string(#call) + ": " + hipGetErrorString(_e) +    \
+                      " (" + __FILE__ + ":" + std::to_string(__LINE__) + ")"); \
+      return -1;                                                              \
+    }                                                                         \
+  } while (0)
+
+#define MR_CHECK(cond, msg)                                                   \
+  do {                                                                        \
+    if (!(cond)) {                                                            \
+      ::mr::set_error(msg);                                                   \
+      return -1;                                                              \
+    }                                                                         \
+  } while (0)
+
+constexpr int kMaxK = 128;        // largest factor count the Gram kernel tiles
+inline int ldk_of(int k) { return (k + 3) & ~3; }   // row stride, 16-B rows
+
+// One wave's unit of Gram work: ratings [begin, begin+len) of one entity's
+// CSR row; slab >= 0 writes a partial record to be combined by slab_reduce.
+struct WorkItem {
+  int64_t begin;
+  int32_t len;
+  int32_t entity;   // local entity index
+  int32_t slab;     // -1: write the entity's normal equations directly
+  int32_t pad;
+};
+
+// Split entity: partial records [slab0, slab0+nslab) sum into `entity`.
+struct SplitItem {
+  int32_t entity;
+  int32_t slab0;
+  int32_t nslab;
+  int32_t pad;
+};
+
+// Destination of normal equations: entity / slab i writes
+//   G  + i*sG  (k rows x ldk)   Gs + i*sV (sum of rows, user side)
+//   C  + i*sV  (rhs)            Cb + i*sS (sum of ratings, user side)
+//   Gn + i*sS  (rating count, user side)
+struct GramDst {
+  float* G;
+  float* Gs;
+  float* C;
+  float* Cb;
+  float* Gn;
+  int64_t sG, sV, sS;
+};
+
+// CG scalar state, device resident (matrix.cpp:456-529 scalars).
+struct CgState {
+  double rr;        // r.r of the current iterate
+  double alpha;
+  double beta;
+  double final_rr;
+  double min_dec;   // min_r_decrease
+  double comm[2];   // local sums exchanged by all-reduce in sharded runs
+  int32_t it;       // iteration counter
+  int32_t fails;    // consecutive beta > 1 - min_dec
+  int32_t done;     // solve finished: every later kernel is a no-op
+  int32_t ret;      // iteration count returned by cg_least_squares
+  int32_t max_it;
+  int32_t n_matvec; // matvec launches that did work (for kernel timing)
+};
+
+enum CgPhase { CG_INIT = 0, CG_ALPHA = 1, CG_BETA = 2 };
+enum CgCtl { CTL_REDUCE = 1, CTL_FINALIZE = 2, CTL_BOTH = 3 };
+enum CgUpd { UPD_INIT = 0, UPD_STEP = 1 };
+
+// Kernel launchers (kernels.hip) ---------------------------------------------
+int launch_gram(hipStream_t s, bool user_side, int k, const WorkItem* work,
+                int64_t n_work, const int32_t* idx, const float* val,
+                const float* F, const float* bias, GramDst direct, GramDst slab);
+int launch_slab_reduce(hipStream_t s, bool user_side, int k,
+                       const SplitItem* split, int64_t n_split,
+                       const float* slab, int64_t rec, GramDst direct);
+int launch_cg_matvec(hipStream_t s, bool user_side, const CgState* st,
+                     int update_p, int64_t E, int k, const float* G,
+                     const float* Gs, const float* Gn, float* v, float* vb,
+                     const float* r, const float* rb, float* y, float* yb,
+                     double* partials, int n_part);
+int launch_cg_update(hipStream_t s, const CgState* st, int mode, int64_t n,
+                     int64_t nb, float* x, float* r, float* p, const float* q,
+                     const float* c, float* xb, float* rb, float* pb,
+                     const float* qb, const float* cb, double* partials,
+                     int n_part);
+int launch_cg_control(hipStream_t s, CgState* st, int phase, int ctl,
+                      const double* partials, int n_part);
+int launch_solve(hipStream_t s, bool user_side, int64_t E, int k, double ridge,
+                 const float* G, const float* Gs, const float* Gn,
+                 const float* C, const float* Cb, float* x, float* xb,
+                 int* nonpd);
+int launch_unpack_factors(hipStream_t s, int64_t rows, int width, int k,
+                          int ldk, const double* src, float* fac, float* bias);
+int launch_pack_factors(hipStream_t s, int64_t rows, int width, int k, int ldk,
+                        const float* fac, const float* bias, double* dst);
+int launch_predict(hipStream_t s, int64_t n, int k, int ldk, const int* uid,
+                   const int* iid, const float* Ufac, const float* Ubias,
+                   const float* Vfac, double* out);
+// General CSR (fp64) CG least squares pieces.
+int launch_spmv_f64(hipStream_t s, int64_t rows, const int64_t* rp,
+                    const int32_t* ci, const double* v, const double* x,
+                    double* y);
+int launch_dot_f64(hipStream_t s, const CgState* st, int64_t n, const double* a,
+                   const double* b, double* partials, int n_part);
+int launch_update_f64(hipStream_t s, const CgState* st, int mode, int64_t n,
+                      double* x, double* r, double* p, const double* q,
+                      const double* c, double* partials, int n_part);
+int launch_p_update_f64(hipStream_t s, const CgState* st, int64_t n,
+                        double* p, const double* r);
+int launch_rows_of(hipStream_t s, int64_t rows, const int64_t* rp,
+                   int32_t* row_of);
+int launch_i32_to_i64(hipStream_t s, int64_t n, const int32_t* in, int64_t* out);
+int launch_validate_ids(hipStream_t s, int64_t n, const int32_t* ids, int32_t lo,
+                        int32_t hi, int* bad);
+
+// CSR construction (csr_build.hip) ------------------------------------------
+// Stable sort of n (key, other, value) triples by key - key_base, which must
+// lie in [0, E).  Produces off[E+1] (int64), idx[n] = other, val[n] (as TV).
+template <typename TV, typename TIn>
+int build_csr(hipStream_t s, int64_t n, int64_t E, const int32_t* d_key,
+              int32_t key_base, const int32_t* d_other, const TIn* d_val, int64_t* off,
+              int32_t* idx, TV* val);
+
+}  // namespace mr

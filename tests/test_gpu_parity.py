@@ -1,0 +1,309 @@
+"""GPU parity: the HIP path (through the C ABI) against the compiled
+reference's golden vectors and the CPU oracle.
+
+Tolerances (fp32 normal equations and CG vectors, fp64 CG scalars):
+  * dense golden fixtures (G2):  max|x - ref| / max|ref| <= 1e-5, same `ret`
+  * MovieLens-shaped sparse fixtures (G3, 60-100 CG iterations per
+    half-step, fp32 round-off accumulates): <= 5e-5, same `ret`
+  * general CG least squares (fp64 on the GPU): <= 1e-9, same iterations
+  * Gram kernel vs fp64 NumPy Gram on sampled entities: <= 2e-5 relative to
+    the block's largest entry
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, load_golden, rel_err
+
+pytestmark = pytest.mark.gpu
+
+DENSE = ["als_dense_38x45_k5.npz", "als_dense_40x45_k3.npz",
+         "als_dense_300x200_k10.npz", "als_dense_200x150_k32.npz"]
+MLSHAPE = ["als_mlshape_k10_it2.npz", "als_mlshape_k10_it4.npz",
+           "als_mlshape_k32_it2.npz", "als_mlshape_k32_it4.npz"]
+
+
+def abi_als(L, d, max_iteration=200, min_r_decrease=0.01):
+    """Call als_from_python exactly as the reference wrapper does, but with the
+    fixture's initial factors."""
+    from movie_recommender_amd import _lib
+    u = np.ascontiguousarray(d["user_ids"], np.int32)
+    i = np.ascontiguousarray(d["item_ids"], np.int32)
+    r = np.ascontiguousarray(d["ratings"], np.float64)
+    U = np.array(d["U0"], np.float64)
+    V = np.array(d["V0"], np.float64)
+    k = int(d["k"])
+    ret = L.als_from_python(u.ctypes.data_as(_lib.IP), i.ctypes.data_as(_lib.IP), len(r),
+                            r.ctypes.data_as(_lib.DP), k, len(U), U.ctypes.data_as(_lib.DP),
+                            len(V), V.ctypes.data_as(_lib.DP), min_r_decrease,
+                            max_iteration, 1)
+    assert ret >= 0, _lib.last_error()
+    return U, V, ret
+
+
+@pytest.mark.parametrize("name", DENSE)
+def test_als_dense_golden(gpu, name):
+    d = load_golden(name)
+    U, V, ret = abi_als(gpu, d)
+    assert ret == int(d["ret"])
+    assert rel_err(U, d["U"]) <= 1e-5, rel_err(U, d["U"])
+    assert rel_err(V, d["V"]) <= 1e-5, rel_err(V, d["V"])
+
+
+@pytest.mark.parametrize("name", MLSHAPE)
+def test_als_mlshape_golden(gpu, name):
+    d = load_golden(name)
+    n_it = int(name.split("_it")[1].split(".")[0])
+    U, V, ret = abi_als(gpu, d, max_iteration=n_it)
+    assert ret == int(d["ret"])
+    assert rel_err(U, d["U"]) <= 5e-5, rel_err(U, d["U"])
+    assert rel_err(V, d["V"]) <= 5e-5, rel_err(V, d["V"])
+
+
+def test_cg_least_squares_golden(gpu):
+    from movie_recommender_amd import _lib
+    d = load_golden("cg_dense_200x50.npz")
+    x = np.array(d["x0"], np.float64)
+    rr = ctypes.c_double(0)
+    rp = np.ascontiguousarray(d["row_ptr"], np.int32)
+    ci = np.ascontiguousarray(d["col_idx"], np.int32)
+    v = np.ascontiguousarray(d["vals"], np.float64)
+    b = np.ascontiguousarray(d["b"], np.float64)
+    for fn in (gpu.cg_least_squares_from_python, gpu.cg_least_squares2_from_python):
+        x = np.array(d["x0"], np.float64)
+        it = fn(len(rp) - 1, int(d["ncols"]), rp.ctypes.data_as(_lib.IP),
+                ci.ctypes.data_as(_lib.IP), v.ctypes.data_as(_lib.DP), len(b),
+                b.ctypes.data_as(_lib.DP), len(x), x.ctypes.data_as(_lib.DP), 0.01, 200,
+                ctypes.byref(rr))
+        assert it == int(d["iterations"])
+        assert rel_err(x, d["x"]) <= 1e-9
+        assert abs(rr.value - float(d["final_rr"])) <= 1e-6 * max(1.0, float(d["final_rr"]))
+
+
+def test_reference_ffi_tests_port(gpu):
+    """cpp/python/cpp_ls_test.py:5-147 through the drop-in module, seeded."""
+    import random
+    from movie_recommender_amd import cpp_ls
+    numpy_state = np.random.get_state()
+    try:
+        np.random.seed(0)
+        random.seed(0)
+        assert cpp_ls.has_dll_loaded()
+        # test_cg_least_squares
+        A = np.random.uniform(-1, 1, (200, 50))
+        x_real = np.random.uniform(-1, 1, (50, 1))
+        b = A.dot(x_real) + np.random.normal(0, 0.1, (200, 1))
+        rows, cols = np.nonzero(A)
+        rp = np.zeros(201, np.int32)
+        np.cumsum(np.bincount(rows, minlength=200), out=rp[1:])
+        x, it, rr = cpp_ls.cg_least_squares(rp, cols.astype(np.int32), A[rows, cols], 50, b)
+        assert np.sum(np.abs(x_real - x)) / 50 < 0.1
+        # test_als (k=5, all users rate all items, 80 % train)
+        from movie_recommender_amd import synth
+        u, i, r, tu, ti, tr = synth.dense_fixture(38, 45, 5, 0.8, seed=0)
+        U, V, its = cpp_ls.als(u, i, r, 5, 38, 45)
+        from oracle.als_oracle import predict
+        assert np.mean(np.abs(predict(U, V, tu, ti, 5) - tr)) < 0.15
+    finally:
+        np.random.set_state(numpy_state)
+
+
+def test_engine_matches_abi_and_is_deterministic(gpu):
+    from movie_recommender_amd.engine import AlsContext
+    d = load_golden("als_dense_300x200_k10.npz")
+    U1, V1, ret1 = abi_als(gpu, d)
+    outs = []
+    for _ in range(2):
+        with AlsContext(d["user_ids"], d["item_ids"], d["ratings"], 10, 300, 200) as ctx:
+            ctx.set_factors(d["U0"], d["V0"])
+            ret = ctx.run()
+            outs.append((ctx.get_factors(), ret))
+    (U2, V2), ret2 = outs[0]
+    (U3, V3), ret3 = outs[1]
+    assert ret1 == ret2 == ret3
+    assert np.array_equal(U1, U2) and np.array_equal(V1, V2)
+    assert np.array_equal(U2, U3) and np.array_equal(V2, V3)   # bitwise reproducible
+
+
+@pytest.mark.parametrize("k", [3, 10, 16, 32, 33, 64, 65, 96, 128])
+def test_gram_kernel_vs_numpy(gpu, k):
+    """Normal equations of both sides against fp64 NumPy, including heavy
+    entities split across waves (chunk 64 forces slabs) and empty entities."""
+    from movie_recommender_amd.engine import AlsContext
+    from oracle import als_oracle as O
+    rng = np.random.default_rng(k)
+    nU, nI = 90, 70
+    n = 4000
+    u = rng.integers(0, nU - 2, n).astype(np.int32)       # last 2 users: no ratings
+    i = (rng.zipf(1.3, n) % (nI - 1)).astype(np.int32)    # heavy items, last item empty
+    key = np.unique(u.astype(np.int64) * nI + i)
+    u = (key // nI).astype(np.int32)
+    i = (key % nI).astype(np.int32)
+    r = rng.normal(0, 1, len(u))
+    U0 = rng.uniform(-1, 1, nU * (k + 1))
+    V0 = rng.uniform(-1, 1, nI * k)
+    with AlsContext(u, i, r, k, nU, nI, gram_chunk=64) as ctx:
+        ctx.set_factors(U0, V0)
+        for side, (Gf, cf) in (("users", O.gram_user(u, i, r, V0, k, nU)),
+                               ("items", O.gram_item(u, i, r, U0, k, nI))):
+            ctx.build_normal_equations(side)
+            ents = np.arange(Gf.shape[0])
+            G, c = ctx.normal_equations(side, ents)
+            scale = np.maximum(np.abs(Gf).max(axis=(1, 2)), 1.0)
+            assert np.max(np.abs(G - Gf).max(axis=(1, 2)) / scale) < 2e-5
+            cs = np.maximum(np.abs(cf).max(axis=1), 1.0)
+            assert np.max(np.abs(c - cf).max(axis=1) / cs) < 2e-5
+            assert np.all(G[-1] == 0) and np.all(c[-1] == 0)   # empty entity
+    from movie_recommender_amd import _lib
+    _lib.check(_lib.lib().mr_set_gram_chunk(2048), "reset chunk")
+
+
+def test_split_vs_unsplit_same_result(gpu):
+    from movie_recommender_amd.engine import AlsContext
+    d = load_golden("als_dense_200x150_k32.npz")
+    res = []
+    for chunk in (64, 4096):
+        with AlsContext(d["user_ids"], d["item_ids"], d["ratings"], 32, 200, 150,
+                        gram_chunk=chunk) as ctx:
+            ctx.set_factors(d["U0"], d["V0"])
+            ret = ctx.run()
+            res.append((ctx.get_factors(), ret))
+    from movie_recommender_amd import _lib
+    _lib.check(_lib.lib().mr_set_gram_chunk(2048), "reset chunk")
+    (Ua, Va), ra = res[0]
+    (Ub, Vb), rb = res[1]
+    assert ra == rb
+    assert rel_err(Ua, Ub) < 1e-5 and rel_err(Va, Vb) < 1e-5
+
+
+def test_empty_entities_keep_their_factors(gpu):
+    """A user / item without ratings has G = 0, c = 0: CG leaves it unchanged,
+    as in the reference (zero rows of A^T A)."""
+    from movie_recommender_amd.engine import AlsContext
+    from oracle import als_oracle as O
+    d = load_golden("als_dense_38x45_k5.npz")
+    k = 5
+    u, i, r = d["user_ids"], d["item_ids"], d["ratings"]
+    nU, nI = 40, 47            # users 38, 39 and items 45, 46 have no ratings
+    rng = np.random.RandomState(4)
+    U0 = rng.uniform(-1, 1, nU * (k + 1))
+    V0 = rng.uniform(-1, 1, nI * k)
+    with AlsContext(u, i, r, k, nU, nI) as ctx:
+        ctx.set_factors(U0, V0)
+        ret = ctx.run()
+        U, V = ctx.get_factors()
+    Uo, Vo, reto, _ = O.als_block(u, i, r, k, U0, V0)
+    assert ret == reto
+    assert rel_err(U, Uo) < 1e-5 and rel_err(V, Vo) < 1e-5
+    assert np.allclose(U[38 * (k + 1):], U0[38 * (k + 1):], atol=1e-7)
+    assert np.allclose(V[45 * k:], V0[45 * k:], atol=1e-7)
+
+
+@pytest.mark.parametrize("k", [10, 64])
+def test_cholesky_mode_vs_oracle(gpu, k):
+    from movie_recommender_amd.engine import AlsContext
+    from movie_recommender_amd import synth
+    from oracle import als_oracle as O
+    u, i, r, *_ = synth.dense_fixture(150, 120, k, 0.9, seed=k)
+    rng = np.random.RandomState(2)
+    U0 = rng.uniform(-1, 1, 150 * (k + 1))
+    V0 = rng.uniform(-1, 1, 120 * k)
+    ridge = 0.1
+    with AlsContext(u, i, r, k, 150, 120, solver="cholesky", ridge=ridge) as ctx:
+        ctx.set_factors(U0, V0)
+        ctx.iterate(2)
+        U, V = ctx.get_factors()
+        st = ctx.stats()
+    assert st["nonpd_users"] == 0 and st["nonpd_items"] == 0
+    Uo, Vo = O.als_exact(u, i, r, k, U0, V0, 2, ridge=ridge)
+    assert rel_err(U, Uo) < 1e-4 and rel_err(V, Vo) < 1e-4
+
+
+def test_band_realistic_heldout_rmse(gpu):
+    """Ill-conditioned MovieLens-shaped data: the reference itself moves by
+    tens of percent across thread counts, so parity is the reference's own
+    held-out RMSE band (G4: 5 seeds x thread counts 1, 2, 8)."""
+    from movie_recommender_amd import synth
+    from movie_recommender_amd.engine import AlsContext
+    from oracle import als_oracle as O
+    from oracle.ref import init_factors
+    with open(os.path.join(GOLDEN, "band_ml100k_k10.json")) as f:
+        band = json.load(f)
+    k = band["k"]
+    rs = synth.movielens_like(band["shape"], k, seed=band["data_seed"],
+                              test_ratio=band["test_ratio"])
+    lo = band["test_rmse_min"] - 3 * band["test_rmse_std"]
+    hi = band["test_rmse_max"] + 3 * band["test_rmse_std"]
+    vals = []
+    for seed in range(3):
+        U0, V0 = init_factors(rs.num_users, rs.num_items, k, seed)
+        with AlsContext(rs.user_ids, rs.item_ids, rs.ratings, k, rs.num_users,
+                        rs.num_items) as ctx:
+            ctx.set_factors(U0, V0)
+            ctx.run()
+            U, V = ctx.get_factors()
+        vals.append(O.rmse(U, V, rs.test_user_ids, rs.test_item_ids, rs.test_ratings, k))
+    assert lo <= np.mean(vals) <= hi, (vals, lo, hi)
+
+
+def test_predict_matches_reference_formula(gpu):
+    from movie_recommender_amd.engine import AlsContext
+    from oracle import als_oracle as O
+    d = load_golden("als_dense_40x45_k3.npz")
+    with AlsContext(d["user_ids"], d["item_ids"], d["ratings"], 3, 40, 45) as ctx:
+        ctx.set_factors(d["U"], d["V"])
+        p = ctx.predict(d["test_user_ids"], d["test_item_ids"])
+    ref = O.predict(d["U"], d["V"], d["test_user_ids"], d["test_item_ids"], 3)
+    assert np.max(np.abs(p - ref)) < 1e-5
+
+
+def test_bad_ids_fail_cleanly(gpu):
+    from movie_recommender_amd import cpp_ls
+    u = np.array([0, 1, 5], np.int32)
+    i = np.array([0, 0, 0], np.int32)
+    with pytest.raises(RuntimeError):
+        cpp_ls.als(u, i, np.ones(3), 2, 2, 1)
+
+
+@pytest.mark.slow
+def test_full_size_gram_sampled(gpu):
+    """BASELINE.json configs[2] size (ML-full shape, k = 64): the Gram kernel
+    on sampled entities (heaviest, lightest, random) against fp64 NumPy, and
+    one CG half-step that must reduce r.r."""
+    from movie_recommender_amd import synth
+    from movie_recommender_amd.engine import AlsContext
+    rs = synth.movielens_like("ml-full", 64)
+    k = 64
+    rng = np.random.default_rng(0)
+    U0 = rng.uniform(-1, 1, rs.num_users * (k + 1))
+    V0 = rng.uniform(-1, 1, rs.num_items * k)
+    with AlsContext(rs.user_ids, rs.item_ids, rs.ratings, k, rs.num_users,
+                    rs.num_items) as ctx:
+        ctx.set_factors(U0, V0)
+        for side in ("users", "items"):
+            ids = rs.user_ids if side == "users" else rs.item_ids
+            other = rs.item_ids if side == "users" else rs.user_ids
+            cnt = np.bincount(ids)
+            ents = np.unique(np.concatenate([np.argsort(cnt)[-3:], np.argsort(cnt)[:3],
+                                             rng.integers(0, len(cnt), 6)])).astype(np.int32)
+            ctx.build_normal_equations(side)
+            G, c = ctx.normal_equations(side, ents)
+            Vm = V0.reshape(-1, k)
+            Um = U0.reshape(-1, k + 1)
+            for t, e in enumerate(ents):
+                sel = ids == e
+                if side == "users":
+                    a = np.hstack([Vm[other[sel]], np.ones((sel.sum(), 1))])
+                    w = rs.ratings[sel]
+                else:
+                    a = Um[other[sel], :k]
+                    w = rs.ratings[sel] - Um[other[sel], k]
+                Gr = a.T @ a
+                cr = a.T @ w
+                assert np.max(np.abs(G[t] - Gr)) / np.max(np.abs(Gr)) < 2e-5
+                assert np.max(np.abs(c[t] - cr)) / max(np.max(np.abs(cr)), 1.0) < 2e-5
+        its, rr = ctx.half_step("users")
+        assert its >= 1 and np.isfinite(rr)
