@@ -55,22 +55,30 @@ def load_data(shape, k, cache_dir="/tmp"):
 
 
 def algorithmic_cost(cls, k, n_users, n_items, n_ratings, ldk):
-    """(bytes, flops) per launch of a kernel class; definitions in DESIGN.md."""
+    """(bytes, flops) per launch of a kernel class; definitions in DESIGN.md.
+
+    Normal equations are stored as upper-triangular 16x16 blocks ("packed16":
+    nbp = nb(nb+1)/2 blocks of 256 floats, nb = ceil(k/16)); the CG matvec's
+    bytes are that storage plus the CG vectors it streams.  Gram flops are the
+    full K x K outer products of SURVEY.md 8(d) F(k) (the kernel computes only
+    the upper blocks, so its MFMA work is nbp*512 flop per rating)."""
     K = k + 1
+    nb = (k + 15) // 16
+    gsz = nb * (nb + 1) // 2 * 256
     if cls == "matvec_users":
         E = n_users
-        g = E * (k * ldk + ldk + 1) * 4            # G_e (S, s, n) read once
+        g = E * (gsz + ldk + 1) * 4               # G_e blocks + Gs row + count
         v = E * (ldk + 1) * 4 * 4                 # p read+write, r read, Ap write
         return g + v, E * 2.0 * K * K
     if cls == "matvec_items":
         E = n_items
-        return E * k * ldk * 4 + E * ldk * 4 * 4, E * 2.0 * k * k
+        return E * gsz * 4 + E * ldk * 4 * 4, E * 2.0 * k * k
     if cls == "gram_users":
-        # per rating: (idx, value) 8 B + gathered item row k*4 B; output E*K^2
-        b = n_ratings * (8 + 4 * k) + n_users * (k * ldk + 2 * ldk + 2) * 4
+        # per rating: (idx, value) 8 B + gathered item row k*4 B; output blocks
+        b = n_ratings * (8 + 4 * k) + n_users * (gsz + 2 * ldk + 2) * 4
         return b, n_ratings * (2.0 * K * K + 2.0 * K)
     if cls == "gram_items":
-        b = n_ratings * (8 + 4 * (k + 1)) + n_items * (k * ldk + ldk) * 4
+        b = n_ratings * (8 + 4 * (k + 1)) + n_items * (gsz + ldk) * 4
         return b, n_ratings * (2.0 * k * k + 2.0 * k)
     if cls == "cg_update":
         E = (n_users * (ldk + 1) + n_items * ldk) / 2.0   # average side
@@ -117,8 +125,8 @@ def cpu_baseline(rs, k, threads, frac, seed=0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--k", type=int, default=64)
     ap.add_argument("--shape", default="ml-full")
     ap.add_argument("--solver", default="cg", choices=["cg", "cholesky"])

@@ -8,7 +8,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "cpp_ls_lib.so")
+LIB_PATH = os.environ.get("MR_LIB_PATH") or os.path.join(HERE, "lib", "cpp_ls_lib.so")
 
 K_NAMES = ["gram_users", "gram_items", "slab_reduce", "matvec_users",
            "matvec_items", "cg_update", "cg_control", "solve"]

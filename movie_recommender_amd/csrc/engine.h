@@ -47,6 +47,9 @@ struct Engine {
   CgState* h_state = nullptr;
   CgState* h_init = nullptr;
   double* h_stage = nullptr;
+  CgMirror* h_mirror = nullptr;   // pinned, host-mapped, coherent
+  CgMirror* d_mirror = nullptr;   // its device address
+  int mirror_seq = 0;
   double* partials = nullptr;
   int* d_flag = nullptr;
   int cur_parts = 1;
@@ -74,7 +77,8 @@ struct Engine {
   bool sharded() const { return has_comm && comm.world > 1; }
   int allreduce_state_slot();
   int allgather_side(bool user);
-  int control(int phase);
+  int control(int phase, int seq);
+  int wait_mirror(int target, CgMirror* out);
   GramDst direct_dst(Side& S);
   GramDst slab_dst(Side& S);
   int gram(Side& S);

@@ -62,6 +62,7 @@ Engine::~Engine() {
     if (h_state) (void)hipHostFree(h_state);
     if (h_init) (void)hipHostFree(h_init);
     if (h_stage) (void)hipHostFree(h_stage);
+    if (h_mirror) (void)hipHostFree(h_mirror);
     for (auto& e : ev_pool) (void)hipEventDestroy(e);
     for (auto& p : pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     (void)hipStreamDestroy(stream);
@@ -161,7 +162,7 @@ int Engine::build_side(Side& S, bool user, int64_t n, const int32_t* d_key,
   S.n_work = (int64_t)work.size();
   S.n_split = (int64_t)split.size();
   S.n_slab = nslab;
-  S.rec = (int64_t)k * ldk + 2 * ldk + 4;
+  S.rec = gsize_of(k) + 2 * ldk + 4;
   if (dalloc(&S.work, S.n_work, stream) || dalloc(&S.split, S.n_split, stream) ||
       dalloc(&S.slab, S.n_slab * S.rec, stream))
     return -1;
@@ -173,7 +174,7 @@ int Engine::build_side(Side& S, bool user, int64_t n, const int32_t* d_key,
                           hipMemcpyHostToDevice, stream));
   // normal equations + CG vectors
   const int64_t ef = S.E * ldk;
-  if (dalloc(&S.G, S.E * (int64_t)k * ldk, stream) || dalloc(&S.C, ef, stream) ||
+  if (dalloc(&S.G, S.E * gsize_of(k), stream) || dalloc(&S.C, ef, stream) ||
       dalloc(&S.r, ef, stream) || dalloc(&S.p, ef, stream) || dalloc(&S.q, ef, stream))
     return -1;
   if (user) {
@@ -211,6 +212,10 @@ int Engine::init(int dev, int k_, int64_t U_, int64_t I_, int64_t n_u,
   MR_HIP(hipHostMalloc((void**)&h_state, sizeof(CgState), hipHostMallocDefault));
   MR_HIP(hipHostMalloc((void**)&h_init, sizeof(CgState), hipHostMallocDefault));
   MR_HIP(hipHostMalloc((void**)&h_stage, 64, hipHostMallocDefault));
+  MR_HIP(hipHostMalloc((void**)&h_mirror, sizeof(CgMirror),
+                       hipHostMallocMapped | hipHostMallocCoherent));
+  memset(h_mirror, 0, sizeof(CgMirror));
+  MR_HIP(hipHostGetDevicePointer((void**)&d_mirror, h_mirror, 0));
   if (dalloc(&d_state, 1, stream) || dalloc(&partials, kMaxParts, stream) ||
       dalloc(&d_flag, 4, stream))
     return -1;
@@ -359,17 +364,47 @@ int Engine::allgather_side(bool user) {
   return 0;
 }
 
-int Engine::control(int phase) {
+int Engine::control(int phase, int seq) {
   hipEvent_t a = nullptr;
   if (tic(MR_K_CG_CONTROL, -1, &a)) return -1;
+  CgMirror* m = seq > 0 ? d_mirror : nullptr;
   if (!sharded()) {
-    if (launch_cg_control(stream, d_state, phase, CTL_BOTH, partials, cur_parts)) return -1;
+    if (launch_cg_control(stream, d_state, phase, CTL_BOTH, partials, cur_parts, m, seq))
+      return -1;
   } else {
     if (launch_cg_control(stream, d_state, phase, CTL_REDUCE, partials, cur_parts)) return -1;
     if (allreduce_state_slot()) return -1;
-    if (launch_cg_control(stream, d_state, phase, CTL_FINALIZE, partials, cur_parts)) return -1;
+    if (launch_cg_control(stream, d_state, phase, CTL_FINALIZE, partials, cur_parts, m, seq))
+      return -1;
   }
   return toc(MR_K_CG_CONTROL, -1, a);
+}
+
+// Spin on the host-mapped mirror until a state with seq >= target has been
+// published.  Checks the stream for errors, and for "stream idle but nothing
+// published" (which would be a bug) instead of hanging.
+int Engine::wait_mirror(int target, CgMirror* out) {
+  long spins = 0;
+  while (true) {
+    const int cur = __atomic_load_n(&h_mirror->seq, __ATOMIC_ACQUIRE);
+    if (cur >= target) {
+      *out = *h_mirror;
+      out->seq = cur;
+      __atomic_thread_fence(__ATOMIC_ACQUIRE);
+      if (__atomic_load_n(&h_mirror->seq, __ATOMIC_ACQUIRE) == cur) return 0;
+      continue;  // a newer state landed while copying: read again
+    }
+    if ((++spins & 1023) == 0) {
+      const hipError_t q = hipStreamQuery(stream);
+      if (q == hipSuccess) {
+        if (__atomic_load_n(&h_mirror->seq, __ATOMIC_ACQUIRE) >= target) continue;
+        MR_CHECK(false, "CG state was not published (stream idle)");
+      }
+      MR_CHECK(q == hipErrorNotReady,
+               std::string("stream error while polling CG state: ") + hipGetErrorString(q));
+    }
+    __builtin_ia32_pause();
+  }
 }
 
 // ----------------------------------------------------------------------------
@@ -378,13 +413,13 @@ int Engine::control(int phase) {
 GramDst Engine::direct_dst(Side& S) {
   GramDst d;
   d.G = S.G; d.Gs = S.Gs; d.C = S.C; d.Cb = S.Cb; d.Gn = S.Gn;
-  d.sG = (int64_t)k * ldk; d.sV = ldk; d.sS = 1;
+  d.sG = gsize_of(k); d.sV = ldk; d.sS = 1;
   return d;
 }
 
 GramDst Engine::slab_dst(Side& S) {
   GramDst d;
-  const int64_t nG = (int64_t)k * ldk;
+  const int64_t nG = gsize_of(k);
   d.G = S.slab; d.Gs = S.slab + nG; d.C = S.slab + nG + ldk;
   d.Cb = S.slab + nG + 2 * ldk; d.Gn = S.slab + nG + 2 * ldk + 1;
   d.sG = d.sV = d.sS = S.rec;
@@ -422,6 +457,12 @@ int Engine::x_ptrs(Side& S, float** xf, float** xb) {
   return 0;
 }
 
+// One global CG solve (cg_least_squares, matrix.cpp:456-529) on the side's
+// block-diagonal normal equations.  Host protocol: every BETA step publishes
+// the CG state to host-mapped memory; iteration t+1 is enqueued before
+// iteration t's state is known only when the known state (after t-1) proves
+// that t cannot terminate (fails == 0, rr far above 1e-6, t+1 < max_it) --
+// so the stream stays busy without launching iterations that would be idle.
 int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr) {
   float *xf, *xb;
   x_ptrs(S, &xf, &xb);
@@ -446,35 +487,50 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr) {
     return -1;
   if (toc(MR_K_CG_UPDATE, -1, a)) return -1;
   cur_parts = kUpdParts;
-  if (control(CG_INIT)) return -1;
-  int t = 0;
-  int chunk_it = 4;
-  while (true) {
-    for (int c = 0; c < chunk_it; ++c, ++t) {
-      if (tic(mv_cls, t, &a)) return -1;
-      if (launch_cg_matvec(stream, user, d_state, t > 0, S.E, k, S.G, S.Gs, S.Gn, S.p,
-                           S.pb, S.r, S.rb, S.q, S.qb, partials, S.n_part_mv))
-        return -1;
-      if (toc(mv_cls, t, a)) return -1;
-      cur_parts = S.n_part_mv;
-      if (control(CG_ALPHA)) return -1;
-      if (tic(MR_K_CG_UPDATE, t, &a)) return -1;
-      if (launch_cg_update(stream, d_state, UPD_STEP, n, nb, xf, S.r, S.p, S.q, S.C, xb,
-                           S.rb, S.pb, S.qb, S.Cb, partials, kUpdParts))
-        return -1;
-      if (toc(MR_K_CG_UPDATE, t, a)) return -1;
-      cur_parts = kUpdParts;
-      if (control(CG_BETA)) return -1;
+  const int seq_init = ++mirror_seq;
+  if (control(CG_INIT, seq_init)) return -1;
+
+  std::vector<int> seq_of;   // publish seq of iteration t's BETA step
+  auto launch_iter = [&](int t) -> int {
+    hipEvent_t ev = nullptr;
+    if (tic(mv_cls, t, &ev)) return -1;
+    if (launch_cg_matvec(stream, user, d_state, t > 0, S.E, k, S.G, S.Gs, S.Gn, S.p, S.pb,
+                         S.r, S.rb, S.q, S.qb, partials, S.n_part_mv))
+      return -1;
+    if (toc(mv_cls, t, ev)) return -1;
+    cur_parts = S.n_part_mv;
+    if (control(CG_ALPHA, 0)) return -1;
+    if (tic(MR_K_CG_UPDATE, t, &ev)) return -1;
+    if (launch_cg_update(stream, d_state, UPD_STEP, n, nb, xf, S.r, S.p, S.q, S.C, xb, S.rb,
+                         S.pb, S.qb, S.Cb, partials, kUpdParts))
+      return -1;
+    if (toc(MR_K_CG_UPDATE, t, ev)) return -1;
+    cur_parts = kUpdParts;
+    seq_of.push_back(++mirror_seq);
+    return control(CG_BETA, seq_of.back());
+  };
+
+  CgMirror ms{};
+  if (wait_mirror(seq_init, &ms)) return -1;
+  int known = -1;            // index of the last iteration whose state is in ms
+  int launched = 0;          // iterations enqueued so far
+  while (!ms.done) {
+    if (launched <= known + 1) {
+      if (launch_iter(launched)) return -1;
+      ++launched;
     }
-    MR_HIP(hipMemcpyAsync(h_state, d_state, sizeof(CgState), hipMemcpyDeviceToHost, stream));
-    MR_HIP(hipStreamSynchronize(stream));
-    if (h_state->done) break;
-    MR_CHECK(t <= max_it + 64, "CG did not terminate");
-    chunk_it = std::min(chunk_it * 2, 16);
+    // speculate one further iteration when iteration known+1 cannot stop
+    if (launched == known + 2 && ms.fails == 0 && ms.rr > 1e-4 && known + 2 < max_it) {
+      if (launch_iter(launched)) return -1;
+      ++launched;
+    }
+    if (wait_mirror(seq_of[known + 1], &ms)) return -1;
+    while (known + 1 < (int)seq_of.size() && seq_of[known + 1] <= ms.seq) ++known;
+    MR_CHECK(launched <= max_it + 2, "CG did not terminate");
   }
-  if (resolve_timing(h_state->n_matvec)) return -1;
-  if (final_rr) *final_rr = h_state->final_rr;
-  return h_state->ret;
+  if (resolve_timing(ms.n_matvec)) return -1;
+  if (final_rr) *final_rr = ms.final_rr;
+  return ms.ret;
 }
 
 int Engine::solve(Side& S) {
@@ -594,12 +650,13 @@ int Engine::get_normal_equations(bool user, int n, const int* ents, double* G, d
   MR_HIP(hipSetDevice(device));
   Side& S = user ? su : si;
   const int K = user ? k + 1 : k;
-  std::vector<float> g((size_t)k * ldk), v(ldk), s(ldk);
+  const int nb = nb16_of(k);
+  std::vector<float> g(gsize_of(k)), v(ldk), s(ldk);
   float cb = 0.f, gn = 0.f;
   for (int t = 0; t < n; ++t) {
     const int64_t e = ents[t];
     MR_CHECK(e >= 0 && e < S.E, "entity out of range");
-    MR_HIP(hipMemcpyAsync(g.data(), S.G + e * k * ldk, (size_t)k * ldk * 4,
+    MR_HIP(hipMemcpyAsync(g.data(), S.G + e * gsize_of(k), gsize_of(k) * 4,
                           hipMemcpyDeviceToHost, stream));
     MR_HIP(hipMemcpyAsync(v.data(), S.C + e * ldk, ldk * 4, hipMemcpyDeviceToHost, stream));
     if (user) {
@@ -613,8 +670,9 @@ int Engine::get_normal_equations(bool user, int n, const int* ents, double* G, d
     for (int i = 0; i < K; ++i) {
       for (int j = 0; j < K; ++j) {
         double val;
-        if (i < k && j < k) val = g[(size_t)i * ldk + j];
-        else if (i < k) val = s[i];
+        if (i < k && j < k) {
+          val = g[packed_offset(i, j, nb)];
+        } else if (i < k) val = s[i];
         else if (j < k) val = s[j];
         else val = gn;
         Ge[i * K + j] = val;

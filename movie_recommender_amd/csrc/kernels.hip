@@ -13,6 +13,8 @@
 //   cg_control       global scalars + stop rules (:488-525)
 //   solve_kernel     exact per-entity Cholesky (north-star "exact" mode)
 // Wave = 64 lanes throughout; no CUDA idioms.
+#include <cstdlib>
+
 #include "mr_internal.h"
 
 namespace mr {
@@ -49,112 +51,192 @@ __device__ __forceinline__ double block_sum_f64(double v, double* sh) {
 }
 
 // ---------------------------------------------------------------------------
-// K1: gather-Gram.  One wave per WorkItem (entity or chunk of a heavy
-// entity).  Rows a_r are gathered from the opposite factor table
-// (row stride ldk floats) and accumulated with v_mfma_f32_32x32x2_f32:
-// lane l supplies a_{r0+(l>>5)}[32b + (l&31)], which is both the A operand
-// (A[i][kk], i = l&31, kk = l>>5) and the B operand (B[kk][j], j = l&31) of
-// the 32x32 block (bi, bj): D += A_bi^T A_bj over 2 ratings per MFMA.  Only
-// the KB(KB+1)/2 upper blocks are computed; the epilogue mirrors them
-// through LDS.  The rhs and (user side) row sums / counts ride along on
-// VALU.  Item side: w = r - U[u][k] (fill_ratings_minus_bias, :1021-1030).
+// K1: gather-Gram.  One wave per WorkItem (an entity, or a chunk of a heavy
+// entity).  Rows a_r are gathered from the opposite factor table (row stride
+// ldk floats) and accumulated with v_mfma_f32_16x16x4_f32: lane l supplies
+// a_{r0+(l>>4)}[16b + (l&15)], which is both the A operand (A[i][kk],
+// i = l&15, kk = l>>4) and the B operand (B[kk][j], j = l&15) of block
+// (bi, bj): D += A_bi^T A_bj over 4 ratings per MFMA.  Only the NB(NB+1)/2
+// upper blocks are computed (k = 64: 10 of 16), and the accumulators are
+// stored as they stand: D[row = 4(l>>4) + reg][col = l&15] is exactly the
+// packed16 block layout, so the epilogue needs no transpose.  The rhs and
+// (user side) row sums / counts ride along on VALU.  Item side:
+// w = r - U[u][k] (fill_ratings_minus_bias, :1021-1030).
+// Rows of UNR steps are gathered before their MFMAs (UNR*NB loads in flight
+// per wave).
 // ---------------------------------------------------------------------------
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 constexpr int GRAM_WAVES = 4;
-constexpr int GRAM_UNR = 4;
 
-template <int KB, bool USER>
+// Per-lane copy of one 64-rating chunk: opposite id and weight.
+struct ChunkRegs {
+  int idx;
+  float w;
+};
+
+template <bool USER>
+__device__ __forceinline__ ChunkRegs load_chunk(const int32_t* __restrict__ idx,
+                                                const float* __restrict__ val,
+                                                const float* __restrict__ bias,
+                                                int64_t begin, int64_t end, int c,
+                                                int lane) {
+  const int64_t jj = begin + 64 * (int64_t)c + lane;
+  const bool ok = jj < end;
+  ChunkRegs r;
+  r.idx = ok ? idx[jj] : -1;
+  r.w = ok ? val[jj] : 0.f;
+  if (!USER) {
+    const float b = bias[ok ? r.idx : 0];
+    r.w = ok ? r.w - b : 0.f;
+  }
+  return r;
+}
+
+// Gather the rows of G steps (4 ratings each) into registers.  Lane l takes
+// row (l>>4) of each step and its NB contiguous floats starting at natural
+// column NB*(l&15): a[u][b] = F[row][NB*(l&15) + b] is the operand of virtual
+// block b.  For NB % 4 == 0 this is NB/4 dwordx4 loads (k = 64: one 1-KiB
+// wave-instruction fetches 4 whole rows).  Padding columns of F (k <= c < ldk)
+// are zero by construction, so only whole segments beyond ldk are masked.
+template <int NB, int G>
+__device__ __forceinline__ void gather_group(float (&a)[G][NB], float (&ww)[G], ChunkRegs cr,
+                                             int step0_in_chunk, int steps_left,
+                                             const float* __restrict__ F, int k, int ldk,
+                                             int q, int col) {
+  const int c0 = NB * col;
+#pragma unroll
+  for (int u = 0; u < G; ++u) {
+    const int src = (4 * (step0_in_chunk + u) + q) & 63;
+    const int ri = __shfl(cr.idx, src, 64);
+    const float wv = __shfl(cr.w, src, 64);
+    const bool ok = (u < steps_left) && (ri >= 0);
+    ww[u] = ok ? wv : 0.f;
+    const int64_t rowb = (int64_t)(ok ? ri : 0) * ldk;
+    if constexpr (NB % 4 == 0) {
+      const bool okv = ok && (c0 < ldk);
+#pragma unroll
+      for (int h = 0; h < NB / 4; ++h) {
+        const float4 v = *reinterpret_cast<const float4*>(F + (okv ? rowb + c0 + 4 * h : 0));
+        a[u][4 * h + 0] = okv ? v.x : 0.f;
+        a[u][4 * h + 1] = okv ? v.y : 0.f;
+        a[u][4 * h + 2] = okv ? v.z : 0.f;
+        a[u][4 * h + 3] = okv ? v.w : 0.f;
+      }
+    } else if constexpr (NB == 2) {
+      const bool okv = ok && (c0 < ldk);
+      const float2 v = *reinterpret_cast<const float2*>(F + (okv ? rowb + c0 : 0));
+      a[u][0] = okv ? v.x : 0.f;
+      a[u][1] = okv ? v.y : 0.f;
+    } else {
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const int c = c0 + b;
+        const bool okc = ok && (c < k);
+        const float v = F[okc ? rowb + c : 0];
+        a[u][b] = okc ? v : 0.f;
+      }
+    }
+  }
+}
+
+template <int NB, int G, bool USER>
+__device__ __forceinline__ void mfma_group(floatx4 (&acc)[NB * (NB + 1) / 2],
+                                           float (&cacc)[NB], float (&sacc)[NB], float& wsum,
+                                           const float (&a)[G][NB], const float (&ww)[G],
+                                           int steps_left) {
+#pragma unroll
+  for (int u = 0; u < G; ++u) {
+    if (u < steps_left) {
+      int t = 0;
+#pragma unroll
+      for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+        for (int bj = bi; bj < NB; ++bj) {
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][bi], a[u][bj], acc[t], 0, 0, 0);
+          ++t;
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      cacc[b] = fmaf(a[u][b], ww[u], cacc[b]);
+      if (USER) sacc[b] += a[u][b];
+    }
+    if (USER) wsum += ww[u];
+  }
+}
+
+template <int NB, int G, bool USER>
 __global__ __launch_bounds__(256) void gram_kernel(
     const WorkItem* __restrict__ work, int64_t n_work,
     const int32_t* __restrict__ idx, const float* __restrict__ val,
     const float* __restrict__ F, const float* __restrict__ bias, int k, int ldk,
     GramDst direct, GramDst slab) {
-  constexpr int T = KB * (KB + 1) / 2;
-  __shared__ float lds_t[GRAM_WAVES][32][33];
+  constexpr int T = NB * (NB + 1) / 2;
+  constexpr int GPC = 16 / G;              // groups per 64-rating chunk
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int64_t wi = (int64_t)blockIdx.x * GRAM_WAVES + wid;
   if (wi >= n_work) return;  // waves are independent: no block barriers below
   const WorkItem w = work[wi];
-  const int half = lane >> 5, col = lane & 31;
+  const int q = lane >> 4, col = lane & 15;
   const int64_t end = w.begin + w.len;
+  const int nst = (w.len + 3) >> 2;              // steps of 4 ratings
+  const int ngroups = (nst + G - 1) / G;
+  const int nchunks = (w.len + 63) >> 6;
 
-  floatx16 acc[T];
+  floatx4 acc[T];
 #pragma unroll
-  for (int t = 0; t < T; ++t)
+  for (int t = 0; t < T; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float cacc[NB], sacc[NB];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-  float cacc[KB], sacc[KB];
-#pragma unroll
-  for (int b = 0; b < KB; ++b) { cacc[b] = 0.f; sacc[b] = 0.f; }
+  for (int b = 0; b < NB; ++b) { cacc[b] = 0.f; sacc[b] = 0.f; }
   float wsum = 0.f;
 
-  for (int64_t j = w.begin; j < end; j += 64) {
-    const int64_t jj = j + lane;
-    const bool okr = jj < end;
-    int my_idx = okr ? idx[jj] : -1;
-    float my_w = okr ? val[jj] : 0.f;
-    if (!USER) {
-      const float b = bias[okr ? my_idx : 0];
-      my_w = okr ? my_w - b : 0.f;
+  // software pipeline: buffers A/B hold the gathered rows of two groups;
+  // chunk registers cur (chunk cc) / nxt (chunk cc+1) feed the gathers.
+  float aA[G][NB], wA[G], aB[G][NB], wB[G];
+  int cc = 0;
+  ChunkRegs cur = load_chunk<USER>(idx, val, bias, w.begin, end, 0, lane);
+  ChunkRegs nxt = load_chunk<USER>(idx, val, bias, w.begin, end, 1, lane);
+  auto issue = [&](float (&a)[G][NB], float (&ww)[G], int g) {
+    const int ch = g / GPC;
+    if (ch == cc + 2) {   // rotate the chunk registers (wave-uniform)
+      cur = nxt;
+      nxt = load_chunk<USER>(idx, val, bias, w.begin, end, cc + 2, lane);
+      ++cc;
     }
-    const int rem = (int)((end - j) < 64 ? (end - j) : 64);
-    const int nsteps = (rem + 1) >> 1;
-    for (int s0 = 0; s0 < nsteps; s0 += GRAM_UNR) {
-      float a[GRAM_UNR][KB];
-      float ww[GRAM_UNR];
-#pragma unroll
-      for (int u = 0; u < GRAM_UNR; ++u) {
-        const int s = s0 + u;
-        const int src = (2 * s + half) & 63;
-        const int ri = __shfl(my_idx, src, 64);
-        const float wv = __shfl(my_w, src, 64);
-        const bool ok = (s < nsteps) && (ri >= 0);
-        ww[u] = ok ? wv : 0.f;
-        const int64_t rowb = (int64_t)(ok ? ri : 0) * ldk;
-#pragma unroll
-        for (int b = 0; b < KB; ++b) {
-          const int c = 32 * b + col;
-          const bool okc = ok && (c < k);
-          const float v = F[okc ? rowb + c : 0];
-          a[u][b] = okc ? v : 0.f;
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < GRAM_UNR; ++u) {
-        int t = 0;
-#pragma unroll
-        for (int bi = 0; bi < KB; ++bi)
-#pragma unroll
-          for (int bj = bi; bj < KB; ++bj) {
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][bi], a[u][bj],
-                                                          acc[t], 0, 0, 0);
-            ++t;
-          }
-#pragma unroll
-        for (int b = 0; b < KB; ++b) {
-          cacc[b] = fmaf(a[u][b], ww[u], cacc[b]);
-          if (USER) sacc[b] += a[u][b];
-        }
-        if (USER) wsum += ww[u];
-      }
-    }
+    const ChunkRegs cr = (ch == cc) ? cur : nxt;
+    gather_group<NB, G>(a, ww, cr, (g % GPC) * G, nst - g * G, F, k, ldk, q, col);
+  };
+  if (ngroups > 0) issue(aA, wA, 0);
+  for (int g = 0; g < ngroups; g += 2) {
+    if (g + 1 < ngroups) issue(aB, wB, g + 1);
+    mfma_group<NB, G, USER>(acc, cacc, sacc, wsum, aA, wA, nst - g * G);
+    if (g + 2 < ngroups) issue(aA, wA, g + 2);
+    if (g + 1 < ngroups)
+      mfma_group<NB, G, USER>(acc, cacc, sacc, wsum, aB, wB, nst - (g + 1) * G);
   }
+  (void)nchunks;
 
   // ---- epilogue -----------------------------------------------------------
 #pragma unroll
-  for (int b = 0; b < KB; ++b) {
+  for (int b = 0; b < NB; ++b) {
+    cacc[b] += __shfl_xor(cacc[b], 16, 64);
     cacc[b] += __shfl_xor(cacc[b], 32, 64);
-    if (USER) sacc[b] += __shfl_xor(sacc[b], 32, 64);
+    if (USER) {
+      sacc[b] += __shfl_xor(sacc[b], 16, 64);
+      sacc[b] += __shfl_xor(sacc[b], 32, 64);
+    }
   }
   const bool to_slab = w.slab >= 0;
   const int64_t di = to_slab ? (int64_t)w.slab : (int64_t)w.entity;
   const GramDst& D = to_slab ? slab : direct;
   float* __restrict__ Gd = D.G + di * D.sG;
   float* __restrict__ Cd = D.C + di * D.sV;
-  if (half == 0) {
+  if (q == 0) {
 #pragma unroll
-    for (int b = 0; b < KB; ++b) {
-      const int c = 32 * b + col;
+    for (int b = 0; b < NB; ++b) {
+      const int c = NB * col + b;   // natural column of virtual (b, col)
       if (c < ldk) {
         Cd[c] = (c < k) ? cacc[b] : 0.f;
         if (USER) D.Gs[di * D.sV + c] = (c < k) ? sacc[b] : 0.f;
@@ -162,101 +244,120 @@ __global__ __launch_bounds__(256) void gram_kernel(
     }
   }
   if (USER) {
-    const float wt = __shfl(wsum, 0, 64) + __shfl(wsum, 32, 64);
+    const float wt = (__shfl(wsum, 0, 64) + __shfl(wsum, 16, 64)) +
+                     (__shfl(wsum, 32, 64) + __shfl(wsum, 48, 64));
     if (lane == 0) {
       D.Cb[di * D.sS] = wt;
       D.Gn[di * D.sS] = (float)w.len;
     }
   }
-  int t = 0;
 #pragma unroll
-  for (int bi = 0; bi < KB; ++bi) {
+  for (int t = 0; t < T; ++t)
 #pragma unroll
-    for (int bj = bi; bj < KB; ++bj) {
-      // direct block (bi, bj): row = 32bi + (r&3) + 8(r>>2) + 4half, col = 32bj + col
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = 32 * bi + (r & 3) + 8 * (r >> 2) + 4 * half;
-        const int cg = 32 * bj + col;
-        if (row < k && cg < ldk) Gd[(int64_t)row * ldk + cg] = acc[t][r];
-      }
-      if (bi != bj) {
-        // mirrored block (bj, bi) through an LDS transpose (stride 33: no
-        // bank conflicts on the column read)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          lds_t[wid][(r & 3) + 8 * (r >> 2) + 4 * half][col] = acc[t][r];
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int r2 = 0; r2 < 16; ++r2) {
-          const int trow = 2 * r2 + half;
-          const float v = lds_t[wid][col][trow];
-          const int row = 32 * bj + trow;
-          const int cg = 32 * bi + col;
-          if (row < k && cg < ldk) Gd[(int64_t)row * ldk + cg] = v;
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
-      ++t;
-    }
-  }
+    for (int r = 0; r < 4; ++r) Gd[t * 256 + (4 * q + r) * 16 + col] = acc[t][r];
 }
 
-template <int KB>
-static int launch_gram_kb(hipStream_t s, bool user_side, int k,
-                          const WorkItem* work, int64_t n_work,
-                          const int32_t* idx, const float* val, const float* F,
-                          const float* bias, GramDst direct, GramDst slab) {
-  if (n_work <= 0) return 0;
+template <int NB, int G>
+static int launch_gram_g(hipStream_t s, bool user_side, int k, const WorkItem* work,
+                         int64_t n_work, const int32_t* idx, const float* val,
+                         const float* F, const float* bias, GramDst direct, GramDst slab) {
   const int64_t grid = (n_work + GRAM_WAVES - 1) / GRAM_WAVES;
   if (user_side)
-    gram_kernel<KB, true><<<dim3((unsigned)grid), dim3(256), 0, s>>>(
+    gram_kernel<NB, G, true><<<dim3((unsigned)grid), dim3(256), 0, s>>>(
         work, n_work, idx, val, F, bias, k, ldk_of(k), direct, slab);
   else
-    gram_kernel<KB, false><<<dim3((unsigned)grid), dim3(256), 0, s>>>(
+    gram_kernel<NB, G, false><<<dim3((unsigned)grid), dim3(256), 0, s>>>(
         work, n_work, idx, val, F, bias, k, ldk_of(k), direct, slab);
   MR_HIP(hipGetLastError());
   return 0;
+}
+
+// Pipeline group size G (steps of 4 ratings gathered per buffer).  Measured
+// on MI355X (tools/gram_bench.py, ML-full shape): G = 4 is best or within 2 %
+// for k = 32, 64, 128; MR_GRAM_G=2|4|8 overrides (tuning).
+static int gram_group_size(int nb) {
+  static int env = -2;
+  if (env == -2) {
+    const char* e = getenv("MR_GRAM_G");
+    env = e ? atoi(e) : -1;
+  }
+  if (env == 2 || env == 4 || env == 8) return env;
+  return 4;
+}
+
+template <int NB>
+static int launch_gram_nb(hipStream_t s, bool user_side, int k, const WorkItem* work,
+                          int64_t n_work, const int32_t* idx, const float* val,
+                          const float* F, const float* bias, GramDst direct, GramDst slab) {
+  if (n_work <= 0) return 0;
+  switch (gram_group_size(NB)) {
+    case 2: return launch_gram_g<NB, 2>(s, user_side, k, work, n_work, idx, val, F, bias, direct, slab);
+    case 4: return launch_gram_g<NB, 4>(s, user_side, k, work, n_work, idx, val, F, bias, direct, slab);
+    default: return launch_gram_g<NB, 8>(s, user_side, k, work, n_work, idx, val, F, bias, direct, slab);
+  }
 }
 
 int launch_gram(hipStream_t s, bool user_side, int k, const WorkItem* work,
                 int64_t n_work, const int32_t* idx, const float* val,
                 const float* F, const float* bias, GramDst direct,
                 GramDst slab) {
-  const int kb = (k + 31) / 32;
-  switch (kb) {
-    case 1: return launch_gram_kb<1>(s, user_side, k, work, n_work, idx, val, F, bias, direct, slab);
-    case 2: return launch_gram_kb<2>(s, user_side, k, work, n_work, idx, val, F, bias, direct, slab);
-    case 3: return launch_gram_kb<3>(s, user_side, k, work, n_work, idx, val, F, bias, direct, slab);
-    case 4: return launch_gram_kb<4>(s, user_side, k, work, n_work, idx, val, F, bias, direct, slab);
+#define MR_GRAM_CASE(NB) \
+  case NB: return launch_gram_nb<NB>(s, user_side, k, work, n_work, idx, val, F, bias, direct, slab);
+  switch (nb16_of(k)) {
+    MR_GRAM_CASE(1) MR_GRAM_CASE(2) MR_GRAM_CASE(3) MR_GRAM_CASE(4)
+    MR_GRAM_CASE(5) MR_GRAM_CASE(6) MR_GRAM_CASE(7) MR_GRAM_CASE(8)
     default: set_error("k > 128 not supported by the Gram kernel"); return -1;
   }
+#undef MR_GRAM_CASE
 }
 
 // ---------------------------------------------------------------------------
 // Combine partial records of split entities, in slab order (deterministic).
-// Record layout: [k*ldk G][ldk Gs][ldk C][Cb][Gn] (+pad).
+// Record layout: [gsize G (packed16)][ldk Gs][ldk C][Cb][Gn] (+pad).
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ void store_rec(const GramDst& d, int64_t e, int64_t t, float v,
+                                          int64_t nG, int ldk, bool user) {
+  if (t < nG) d.G[e * d.sG + t] = v;
+  else if (t < nG + ldk) { if (user) d.Gs[e * d.sV + (t - nG)] = v; }
+  else if (t < nG + 2 * ldk) d.C[e * d.sV + (t - nG - ldk)] = v;
+  else if (t == nG + 2 * ldk) { if (user) d.Cb[e * d.sS] = v; }
+  else if (t == nG + 2 * ldk + 1) { if (user) d.Gn[e * d.sS] = v; }
+}
+
+// grid = (split entities, record float4 chunks); each thread sums one float4
+// of the record over the entity's slabs with 4 independent accumulators that
+// are combined in a fixed order (reproducible).
 template <bool USER>
 __global__ __launch_bounds__(256) void slab_reduce_kernel(
     const SplitItem* __restrict__ split, const float* __restrict__ slab,
     int64_t rec, int k, int ldk, GramDst direct) {
   const SplitItem sp = split[blockIdx.x];
-  const int64_t nG = (int64_t)k * ldk;
+  const int64_t nG = gsize_of(k);
   const int64_t used = nG + 2 * ldk + 2;
-  for (int64_t t = threadIdx.x; t < used; t += blockDim.x) {
-    const bool isGs = t >= nG && t < nG + ldk;
-    const bool isCb = t == nG + 2 * ldk;
-    const bool isGn = t == nG + 2 * ldk + 1;
-    if (!USER && (isGs || isCb || isGn)) continue;
-    float sum = 0.f;
-    for (int q = 0; q < sp.nslab; ++q) sum += slab[(int64_t)(sp.slab0 + q) * rec + t];
-    const int64_t e = sp.entity;
-    if (t < nG) direct.G[e * direct.sG + t] = sum;
-    else if (isGs) direct.Gs[e * direct.sV + (t - nG)] = sum;
-    else if (t < nG + 2 * ldk) direct.C[e * direct.sV + (t - nG - ldk)] = sum;
-    else if (isCb) direct.Cb[e * direct.sS] = sum;
-    else direct.Gn[e * direct.sS] = sum;
+  const int64_t t4 = (int64_t)blockIdx.y * blockDim.x + threadIdx.x;
+  if (t4 * 4 >= used) return;
+  const float4* base = reinterpret_cast<const float4*>(slab + (int64_t)sp.slab0 * rec) + t4;
+  const int64_t rs4 = rec / 4;
+  float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0, a3 = a0;
+  int q = 0;
+  for (; q + 4 <= sp.nslab; q += 4) {
+    const float4 v0 = base[(q + 0) * rs4], v1 = base[(q + 1) * rs4];
+    const float4 v2 = base[(q + 2) * rs4], v3 = base[(q + 3) * rs4];
+    a0.x += v0.x; a0.y += v0.y; a0.z += v0.z; a0.w += v0.w;
+    a1.x += v1.x; a1.y += v1.y; a1.z += v1.z; a1.w += v1.w;
+    a2.x += v2.x; a2.y += v2.y; a2.z += v2.z; a2.w += v2.w;
+    a3.x += v3.x; a3.y += v3.y; a3.z += v3.z; a3.w += v3.w;
+  }
+  for (; q < sp.nslab; ++q) {
+    const float4 v0 = base[q * rs4];
+    a0.x += v0.x; a0.y += v0.y; a0.z += v0.z; a0.w += v0.w;
+  }
+  const float r[4] = {(a0.x + a1.x) + (a2.x + a3.x), (a0.y + a1.y) + (a2.y + a3.y),
+                      (a0.z + a1.z) + (a2.z + a3.z), (a0.w + a1.w) + (a2.w + a3.w)};
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int64_t t = t4 * 4 + c;
+    if (t < used) store_rec(direct, sp.entity, t, r[c], nG, ldk, USER);
   }
 }
 
@@ -264,29 +365,31 @@ int launch_slab_reduce(hipStream_t s, bool user_side, int k,
                        const SplitItem* split, int64_t n_split,
                        const float* slab, int64_t rec, GramDst direct) {
   if (n_split <= 0) return 0;
+  const int ldk = ldk_of(k);
+  const int64_t used4 = (gsize_of(k) + 2 * ldk + 2 + 3) / 4;
+  const dim3 grid((unsigned)n_split, (unsigned)((used4 + 255) / 256));
   if (user_side)
-    slab_reduce_kernel<true><<<dim3((unsigned)n_split), dim3(256), 0, s>>>(
-        split, slab, rec, k, ldk_of(k), direct);
+    slab_reduce_kernel<true><<<grid, dim3(256), 0, s>>>(split, slab, rec, k, ldk, direct);
   else
-    slab_reduce_kernel<false><<<dim3((unsigned)n_split), dim3(256), 0, s>>>(
-        split, slab, rec, k, ldk_of(k), direct);
+    slab_reduce_kernel<false><<<grid, dim3(256), 0, s>>>(split, slab, rec, k, ldk, direct);
   MR_HIP(hipGetLastError());
   return 0;
 }
 
 // ---------------------------------------------------------------------------
-// K2: batched block GEMV y_e = G_e v_e (+ bias row/col on the user side),
-// with the CG direction update v = -r + beta v fused in front (matrix.cpp:521
-// of the previous iteration) and the v.y partial dot behind (:497).
-// One wave per entity, grid-stride over entities with a fixed grid so the
-// partial sums are reproducible.  G_e rows are read as float4: lane l owns
-// columns 4(l % LPR) .. +3 of row ro = l / LPR, LPR = ldk/4, RPI = 64/LPR
-// rows per wave-instruction (k=64: 16 lanes per row, 1 KiB per load).
-// G is symmetric, so row j of G_e equals column j: y = sum_j G[j][:] v_j.
+// K2: batched block GEMV y_e = G_e v_e on packed16 storage (+ bias row/col on
+// the user side), with the CG direction update v = -r + beta v fused in front
+// (matrix.cpp:521 of the previous iteration) and the v.y partial dot behind
+// (:497).  One wave per entity, grid-stride with a fixed grid so partial sums
+// are reproducible.  Each stored 16x16 block T(bi,bj) is ONE float4 load per
+// lane (1 KiB per wave-instruction): lane l holds T[l>>2][4(l&3) .. +3] and
+// accumulates the row product T v_bj into y_bi and, for bi < bj, the column
+// product T^T v_bi into y_bj; the 4-lane row partials and 16-lane column
+// partials are combined once per entity through LDS in a fixed order.
 // ---------------------------------------------------------------------------
 constexpr int MV_WAVES = 4;
 
-template <bool USER>
+template <int NB, bool USER>
 __global__ __launch_bounds__(256) void cg_matvec_kernel(
     const CgState* __restrict__ st, int update_p, int64_t E, int k, int ldk,
     const float* __restrict__ G, const float* __restrict__ Gs,
@@ -294,26 +397,30 @@ __global__ __launch_bounds__(256) void cg_matvec_kernel(
     const float* __restrict__ r, const float* __restrict__ rb,
     float* __restrict__ y, float* __restrict__ yb, double* __restrict__ partials) {
   if (st->done) return;
-  __shared__ float pv[MV_WAVES][kMaxK];
-  __shared__ float4 red[MV_WAVES][64];
+  constexpr int T = NB * (NB + 1) / 2;
+  constexpr int NP = 16 * NB;
+  constexpr int CST = 68;   // float4 stride of a column-partial row (+16 floats: no bank clash)
+  __shared__ float pv[MV_WAVES][NP];
+  __shared__ float redR[MV_WAVES][NB][64];
+  __shared__ float4 redC[MV_WAVES][NB][CST];
   __shared__ double sh[MV_WAVES];
   const float beta = (float)st->beta;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int LPR = ldk >> 2;
-  const int RPI = 64 / LPR;
-  const int ro = lane / LPR, cgp = lane - ro * LPR;
-  const bool act = ro < RPI;
+  const int rr = lane >> 2, c4 = (lane & 3) * 4;
   double dsum = 0.0;
   for (int64_t e = (int64_t)blockIdx.x * MV_WAVES + wid; e < E;
        e += (int64_t)gridDim.x * MV_WAVES) {
     float* ve = v + e * ldk;
-    for (int i = lane; i < ldk; i += 64) {
-      float vi = ve[i];
-      if (update_p) {
-        vi = fmaf(beta, vi, -r[e * ldk + i]);
-        ve[i] = vi;
+    for (int i = lane; i < NP; i += 64) {   // i: natural index; stored virtual
+      float vi = 0.f;
+      if (i < ldk) {
+        vi = ve[i];
+        if (update_p) {
+          vi = fmaf(beta, vi, -r[e * ldk + i]);
+          ve[i] = vi;
+        }
       }
-      pv[wid][i] = vi;
+      pv[wid][virt_of(i, NB)] = vi;
     }
     float vbias = 0.f;
     if (USER) {
@@ -324,49 +431,71 @@ __global__ __launch_bounds__(256) void cg_matvec_kernel(
       }
     }
     __builtin_amdgcn_wave_barrier();
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4* __restrict__ Ge = reinterpret_cast<const float4*>(G + e * (int64_t)k * ldk);
-    if (act) {
-      int j = ro;
-#pragma unroll 4
-      for (; j < k; j += RPI) {
-        const float4 g = Ge[(int64_t)j * LPR + cgp];
-        const float pj = pv[wid][j];
-        acc.x = fmaf(g.x, pj, acc.x);
-        acc.y = fmaf(g.y, pj, acc.y);
-        acc.z = fmaf(g.z, pj, acc.z);
-        acc.w = fmaf(g.w, pj, acc.w);
+    float accR[NB];
+    float4 accC[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      accR[b] = 0.f;
+      accC[b] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const float4* __restrict__ Ge = reinterpret_cast<const float4*>(G + e * (int64_t)T * 256);
+    int t = 0;
+#pragma unroll
+    for (int bi = 0; bi < NB; ++bi) {
+      const float pi = pv[wid][16 * bi + rr];
+#pragma unroll
+      for (int bj = bi; bj < NB; ++bj) {
+        const float4 g = Ge[t * 64 + lane];
+        const float4 pj = *reinterpret_cast<const float4*>(&pv[wid][16 * bj + c4]);
+        float s0 = accR[bi];
+        s0 = fmaf(g.x, pj.x, s0);
+        s0 = fmaf(g.y, pj.y, s0);
+        s0 = fmaf(g.z, pj.z, s0);
+        s0 = fmaf(g.w, pj.w, s0);
+        accR[bi] = s0;
+        if (bi != bj) {
+          accC[bj].x = fmaf(g.x, pi, accC[bj].x);
+          accC[bj].y = fmaf(g.y, pi, accC[bj].y);
+          accC[bj].z = fmaf(g.z, pi, accC[bj].z);
+          accC[bj].w = fmaf(g.w, pi, accC[bj].w);
+        }
+        ++t;
       }
     }
-    red[wid][lane] = acc;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      redR[wid][b][lane] = accR[b];
+      redC[wid][b][lane] = accC[b];
+    }
     __builtin_amdgcn_wave_barrier();
     double d = 0.0;
     float ybp = 0.f;
-    if (lane < LPR) {
-      float4 s = red[wid][lane];
-      for (int q = 1; q < RPI; ++q) {
-        const float4 t = red[wid][q * LPR + lane];
-        s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
-      }
-      const int c0 = 4 * lane;
+    for (int o = lane; o < NP; o += 64) {   // o: virtual index
+      const int n = nat_of(o, NB);
+      if (n >= k) continue;
+      const int b = o >> 4, ii = o & 15;
+      const float* R = &redR[wid][b][4 * ii];
+      float yo = (R[0] + R[1]) + (R[2] + R[3]);
+      const float* C = reinterpret_cast<const float*>(&redC[wid][b][0]) + ii;
+      float sc = 0.f;
+#pragma unroll
+      for (int qq = 0; qq < 16; ++qq) sc += C[16 * qq];
+      yo += sc;
       if (USER) {
-        const float4 g4 = reinterpret_cast<const float4*>(Gs + e * ldk)[lane];
-        s.x = fmaf(g4.x, vbias, s.x);
-        s.y = fmaf(g4.y, vbias, s.y);
-        s.z = fmaf(g4.z, vbias, s.z);
-        s.w = fmaf(g4.w, vbias, s.w);
-        ybp = g4.x * pv[wid][c0] + g4.y * pv[wid][c0 + 1] + g4.z * pv[wid][c0 + 2] +
-              g4.w * pv[wid][c0 + 3];
+        const float gs = Gs[e * ldk + n];
+        yo = fmaf(gs, vbias, yo);
+        ybp = fmaf(gs, pv[wid][o], ybp);
       }
-      reinterpret_cast<float4*>(y + e * ldk)[lane] = s;
-      d = (double)s.x * pv[wid][c0] + (double)s.y * pv[wid][c0 + 1] +
-          (double)s.z * pv[wid][c0 + 2] + (double)s.w * pv[wid][c0 + 3];
+      y[e * ldk + n] = yo;
+      d += (double)yo * pv[wid][o];
     }
     if (USER) {
       const float yb_s = wave_sum_f32(ybp);
       const float ybv = fmaf(Gn[e], vbias, yb_s);
-      if (lane == 0) yb[e] = ybv;
-      if (lane == 0) d += (double)ybv * vbias;
+      if (lane == 0) {
+        yb[e] = ybv;
+        d += (double)ybv * vbias;
+      }
     }
     dsum += wave_sum_f64(d);
     __builtin_amdgcn_wave_barrier();
@@ -375,20 +504,38 @@ __global__ __launch_bounds__(256) void cg_matvec_kernel(
   if (threadIdx.x == 0) partials[blockIdx.x] = tot;
 }
 
+template <int NB>
+static int launch_matvec_nb(hipStream_t s, bool user_side, const CgState* st, int update_p,
+                            int64_t E, int k, const float* G, const float* Gs,
+                            const float* Gn, float* v, float* vb, const float* r,
+                            const float* rb, float* y, float* yb, double* partials,
+                            int n_part) {
+  if (user_side)
+    cg_matvec_kernel<NB, true><<<dim3(n_part), dim3(256), 0, s>>>(
+        st, update_p, E, k, ldk_of(k), G, Gs, Gn, v, vb, r, rb, y, yb, partials);
+  else
+    cg_matvec_kernel<NB, false><<<dim3(n_part), dim3(256), 0, s>>>(
+        st, update_p, E, k, ldk_of(k), G, Gs, Gn, v, vb, r, rb, y, yb, partials);
+  MR_HIP(hipGetLastError());
+  return 0;
+}
+
 int launch_cg_matvec(hipStream_t s, bool user_side, const CgState* st,
                      int update_p, int64_t E, int k, const float* G,
                      const float* Gs, const float* Gn, float* v, float* vb,
                      const float* r, const float* rb, float* y, float* yb,
                      double* partials, int n_part) {
   if (n_part <= 0) return 0;
-  if (user_side)
-    cg_matvec_kernel<true><<<dim3(n_part), dim3(256), 0, s>>>(
-        st, update_p, E, k, ldk_of(k), G, Gs, Gn, v, vb, r, rb, y, yb, partials);
-  else
-    cg_matvec_kernel<false><<<dim3(n_part), dim3(256), 0, s>>>(
-        st, update_p, E, k, ldk_of(k), G, Gs, Gn, v, vb, r, rb, y, yb, partials);
-  MR_HIP(hipGetLastError());
-  return 0;
+#define MR_MV_CASE(NB)                                                               \
+  case NB:                                                                           \
+    return launch_matvec_nb<NB>(s, user_side, st, update_p, E, k, G, Gs, Gn, v, vb, r, \
+                                rb, y, yb, partials, n_part);
+  switch (nb16_of(k)) {
+    MR_MV_CASE(1) MR_MV_CASE(2) MR_MV_CASE(3) MR_MV_CASE(4)
+    MR_MV_CASE(5) MR_MV_CASE(6) MR_MV_CASE(7) MR_MV_CASE(8)
+    default: set_error("k > 128 not supported by the CG matvec"); return -1;
+  }
+#undef MR_MV_CASE
 }
 
 // ---------------------------------------------------------------------------
@@ -474,9 +621,22 @@ int launch_cg_update(hipStream_t s, const CgState* st, int mode, int64_t n,
 // ctl: CTL_REDUCE sums the local partials into st->comm[0] (sharded runs
 // all-reduce that slot next); CTL_FINALIZE applies the rules from comm[0].
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ void publish(const CgState* st, CgMirror* m, int seq) {
+  if (!m) return;
+  m->done = st->done;
+  m->fails = st->fails;
+  m->it = st->it;
+  m->ret = st->ret;
+  m->n_matvec = st->n_matvec;
+  m->rr = st->rr;
+  m->final_rr = st->final_rr;
+  __threadfence_system();
+  __hip_atomic_store(&m->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ __launch_bounds__(256) void cg_control_kernel(
     CgState* __restrict__ st, int phase, int ctl,
-    const double* __restrict__ partials, int n_part) {
+    const double* __restrict__ partials, int n_part, CgMirror* mirror, int seq) {
   if (phase != CG_INIT && st->done) return;
   __shared__ double sh[4];
   if (ctl & CTL_REDUCE) {
@@ -495,6 +655,7 @@ __global__ __launch_bounds__(256) void cg_control_kernel(
     st->done = 0;
     st->ret = 0;
     if (st->max_it <= 0 || s < 1e-6) st->done = 1;
+    publish(st, mirror, seq);
   } else if (phase == CG_ALPHA) {
     st->alpha = st->rr / s;
     st->n_matvec += 1;
@@ -508,20 +669,22 @@ __global__ __launch_bounds__(256) void cg_control_kernel(
     if (st->fails >= 2) {
       st->done = 1;
       st->ret = st->it;
-      return;
+    } else {
+      st->rr = rr2;
+      st->it += 1;
+      if (st->it >= st->max_it || rr2 < 1e-6) {
+        st->done = 1;
+        st->ret = st->it;
+      }
     }
-    st->rr = rr2;
-    st->it += 1;
-    if (st->it >= st->max_it || rr2 < 1e-6) {
-      st->done = 1;
-      st->ret = st->it;
-    }
+    publish(st, mirror, seq);
   }
 }
 
 int launch_cg_control(hipStream_t s, CgState* st, int phase, int ctl,
-                      const double* partials, int n_part) {
-  cg_control_kernel<<<dim3(1), dim3(256), 0, s>>>(st, phase, ctl, partials, n_part);
+                      const double* partials, int n_part, CgMirror* mirror, int seq) {
+  cg_control_kernel<<<dim3(1), dim3(256), 0, s>>>(st, phase, ctl, partials, n_part,
+                                                  mirror, seq);
   MR_HIP(hipGetLastError());
   return 0;
 }
@@ -544,11 +707,12 @@ __global__ __launch_bounds__(256) void solve_kernel(
   double* b = sm + K * K;    // K
   __shared__ int bad;
   const int64_t e = blockIdx.x;
-  const float* Ge = G + e * (int64_t)k * ldk;
+  const int nb = nb16_of(k);
+  const float* Ge = G + e * gsize_of(k);
   for (int t = threadIdx.x; t < K * K; t += blockDim.x) {
     const int i = t / K, j = t - (t / K) * K;
     double v;
-    if (i < k && j < k) v = Ge[(int64_t)i * ldk + j];
+    if (i < k && j < k) v = Ge[packed_offset(i, j, nb)];
     else if (i < k) v = Gs[e * ldk + i];           // j == k
     else if (j < k) v = Gs[e * ldk + j];           // i == k
     else v = Gn[e];

@@ -32,6 +32,30 @@ const char* last_error();
 constexpr int kMaxK = 128;        // largest factor count the Gram kernel tiles
 inline int ldk_of(int k) { return (k + 3) & ~3; }   // row stride, 16-B rows
 
+// Normal-equation storage ("packed16"): the k x k block G_e (in the virtual
+// index order below) is cut into 16 x 16 blocks and only the upper-triangular
+// blocks (bi <= bj) are stored, row-major inside each block, blocks in
+// row-major upper order.  Rows/cols >= k are zero.  k = 64: 10 blocks =
+// 2,560 floats instead of 4,096.
+__host__ __device__ inline int nb16_of(int k) { return (k + 15) / 16; }
+__host__ __device__ inline int nbp_of(int k) { return nb16_of(k) * (nb16_of(k) + 1) / 2; }
+__host__ __device__ inline int64_t gsize_of(int k) { return (int64_t)nbp_of(k) * 256; }
+__host__ __device__ inline int blk_index(int bi, int bj, int nb) {
+  return bi * nb - bi * (bi - 1) / 2 + (bj - bi);
+}
+// Blocks are formed over a permuted ("virtual") factor index so that every
+// lane of the Gram kernel gathers NB contiguous floats of a row (one dwordx4
+// for k = 64): virtual v = 16*b + i  <->  natural n = NB*i + b.
+__host__ __device__ inline int virt_of(int n, int nb) { return 16 * (n % nb) + n / nb; }
+__host__ __device__ inline int nat_of(int v, int nb) { return nb * (v & 15) + (v >> 4); }
+// Stored element for natural (i, j) of a packed16 G_e, -1 if outside k.
+__host__ __device__ inline int64_t packed_offset(int i, int j, int nb) {
+  int vi = virt_of(i, nb), vj = virt_of(j, nb);
+  if ((vi >> 4) > (vj >> 4)) { const int t = vi; vi = vj; vj = t; }
+  const int bi = vi >> 4, bj = vj >> 4;
+  return (int64_t)blk_index(bi, bj, nb) * 256 + (vi & 15) * 16 + (vj & 15);
+}
+
 // One wave's unit of Gram work: ratings [begin, begin+len) of one entity's
 // CSR row; slab >= 0 writes a partial record to be combined by slab_reduce.
 struct WorkItem {
@@ -51,7 +75,7 @@ struct SplitItem {
 };
 
 // Destination of normal equations: entity / slab i writes
-//   G  + i*sG  (k rows x ldk)   Gs + i*sV (sum of rows, user side)
+//   G  + i*sG  (packed16 blocks) Gs + i*sV (sum of rows, user side)
 //   C  + i*sV  (rhs)            Cb + i*sS (sum of ratings, user side)
 //   Gn + i*sS  (rating count, user side)
 struct GramDst {
@@ -79,6 +103,20 @@ struct CgState {
   int32_t n_matvec; // matvec launches that did work (for kernel timing)
 };
 
+// Host-visible copy of the CG state, written by cg_control into pinned,
+// host-mapped coherent memory after every INIT/BETA step (seq last, with a
+// system-scope release), so the host can poll it without a stream sync.
+struct CgMirror {
+  int32_t seq;
+  int32_t done;
+  int32_t fails;
+  int32_t it;
+  int32_t ret;
+  int32_t n_matvec;
+  double rr;
+  double final_rr;
+};
+
 enum CgPhase { CG_INIT = 0, CG_ALPHA = 1, CG_BETA = 2 };
 enum CgCtl { CTL_REDUCE = 1, CTL_FINALIZE = 2, CTL_BOTH = 3 };
 enum CgUpd { UPD_INIT = 0, UPD_STEP = 1 };
@@ -101,7 +139,8 @@ int launch_cg_update(hipStream_t s, const CgState* st, int mode, int64_t n,
                      const float* qb, const float* cb, double* partials,
                      int n_part);
 int launch_cg_control(hipStream_t s, CgState* st, int phase, int ctl,
-                      const double* partials, int n_part);
+                      const double* partials, int n_part, CgMirror* mirror = nullptr,
+                      int seq = 0);
 int launch_solve(hipStream_t s, bool user_side, int64_t E, int k, double ridge,
                  const float* G, const float* Gs, const float* Gn,
                  const float* C, const float* Cb, float* x, float* xb,
