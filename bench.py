@@ -150,10 +150,14 @@ def main():
         dist = tdist
 
     from movie_recommender_amd.engine import AlsContext
-    from movie_recommender_amd.distributed import TorchComm, sharded_context
+    from movie_recommender_amd.distributed import sharded_context
 
     t0 = time.perf_counter()
+    if dist is not None and rank != 0:
+        dist.barrier()            # rank 0 generates (or loads) the data first
     rs = load_data(args.shape, args.k)
+    if dist is not None and rank == 0:
+        dist.barrier()
     k = args.k
     log(f"[bench] data {args.shape} k={k}: N={rs.n} users={rs.num_users} "
         f"items={rs.num_items} ({time.perf_counter() - t0:.1f} s)")
@@ -163,9 +167,8 @@ def main():
 
     t0 = time.perf_counter()
     if world > 1:
-        comm = TorchComm(device=f"cuda:{local_rank}")
         ctx = sharded_context(rs.user_ids, rs.item_ids, rs.ratings, k, rs.num_users,
-                              rs.num_items, local_rank, comm, solver=args.solver,
+                              rs.num_items, local_rank, "rccl", solver=args.solver,
                               ridge=args.ridge)
     else:
         ctx = AlsContext(rs.user_ids, rs.item_ids, rs.ratings, k, rs.num_users,

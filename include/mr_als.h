@@ -99,6 +99,15 @@ mr_als* mr_als_create_shard(int device, int k, int num_users, int num_items,
 int mr_als_set_comm(mr_als* ctx, const mr_comm* comm,
                     const long long* user_begin, const long long* item_begin);
 
+/* Native RCCL collectives (over xGMI) instead of callbacks: rank 0 creates
+ * an id with mr_rccl_unique_id and every rank passes the same 128 bytes.
+ * All ranks must call mr_als_set_rccl concurrently (it builds the RCCL
+ * communicator).  The CG scalars are then all-reduced on the device stream
+ * and factor shards exchanged by grouped in-place broadcasts. */
+int mr_rccl_unique_id(unsigned char out[128]);
+int mr_als_set_rccl(mr_als* ctx, const unsigned char id[128], int rank, int world,
+                    const long long* user_begin, const long long* item_begin);
+
 void mr_als_destroy(mr_als* ctx);
 
 /* Factor tables in the reference layout: U[num_users*(k+1)] (row = k factors,

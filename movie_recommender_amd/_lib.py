@@ -89,6 +89,9 @@ SIGNATURES = {
                                  ctypes.c_longlong, IP, IP, DP,
                                  ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "mr_als_set_comm": (ctypes.c_int, [VP, ctypes.POINTER(MrComm), LLP, LLP]),
+    "mr_rccl_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
+    "mr_als_set_rccl": (ctypes.c_int, [VP, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                       LLP, LLP]),
     "mr_als_destroy": (None, [VP]),
     "mr_als_set_factors": (ctypes.c_int, [VP, DP, DP]),
     "mr_als_get_factors": (ctypes.c_int, [VP, DP, DP]),

@@ -5,7 +5,10 @@
 // (2) The device-resident engine API (include/mr_als.h).
 // No torch types, plain pointers and sizes; failures return <0 / NULL and
 // leave a message in mr_last_error() (also printed to stderr).
+#include <rccl/rccl.h>
+
 #include <cstdlib>
+#include <cstring>
 #include <new>
 
 #include "../../include/cpp_ls_lib.h"
@@ -135,6 +138,25 @@ int mr_als_set_comm(mr_als* ctx, const mr_comm* comm, const long long* user_begi
     ctx->eng.row_begin_u.assign(user_begin, user_begin + comm->world + 1);
     ctx->eng.row_begin_i.assign(item_begin, item_begin + comm->world + 1);
     return 0;
+  });
+}
+
+int mr_rccl_unique_id(unsigned char out[128]) {
+  return guarded([&]() -> int {
+    ncclUniqueId id;
+    MR_CHECK(ncclGetUniqueId(&id) == ncclSuccess, "ncclGetUniqueId failed");
+    memcpy(out, id.internal, 128);
+    return 0;
+  });
+}
+
+int mr_als_set_rccl(mr_als* ctx, const unsigned char id[128], int rank, int world,
+                    const long long* user_begin, const long long* item_begin) {
+  MR_CHECK(ctx && id, "null argument");
+  return guarded([&]() -> int {
+    ctx->eng.row_begin_u.assign(user_begin, user_begin + world + 1);
+    ctx->eng.row_begin_i.assign(item_begin, item_begin + world + 1);
+    return ctx->eng.set_rccl(id, rank, world);
   });
 }
 

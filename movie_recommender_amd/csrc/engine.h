@@ -60,7 +60,9 @@ struct Engine {
   std::vector<hipEvent_t> ev_pool;
   std::vector<Pending> pending;
   mr_stats stats{};
-  // sharded runs
+  // sharded runs: native RCCL communicator (ncclComm_t) or host callbacks
+  void* rccl = nullptr;
+  int rccl_world = 1, rccl_rank = 0;
   bool has_comm = false;
   mr_comm comm{};
   std::vector<long long> row_begin_u, row_begin_i;
@@ -74,7 +76,10 @@ struct Engine {
                  const int32_t* d_other, const double* d_r);
   int set_factors(const double* hU, const double* hV);
   int get_factors(double* hU, double* hV);
-  bool sharded() const { return has_comm && comm.world > 1; }
+  // RCCL attached (any world size, so the collective path is exercised even
+  // single-rank) or host callbacks with more than one rank.
+  bool sharded() const { return rccl != nullptr || (has_comm && comm.world > 1); }
+  int set_rccl(const unsigned char* id, int rank, int world);
   int allreduce_state_slot();
   int allgather_side(bool user);
   int control(int phase, int seq);

@@ -15,6 +15,8 @@
 #include <mutex>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "engine.h"
 
 namespace mr {
@@ -65,6 +67,7 @@ Engine::~Engine() {
     if (h_mirror) (void)hipHostFree(h_mirror);
     for (auto& e : ev_pool) (void)hipEventDestroy(e);
     for (auto& p : pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
+    if (rccl) (void)ncclCommDestroy((ncclComm_t)rccl);
     (void)hipStreamDestroy(stream);
   }
 }
@@ -321,8 +324,35 @@ int Engine::get_factors(double* hU, double* hV) {
 // ----------------------------------------------------------------------------
 // collectives (sharded runs); host-staged callbacks
 // ----------------------------------------------------------------------------
+#define MR_NCCL(call)                                                        \
+  do {                                                                       \
+    ncclResult_t _r = (call);                                                \
+    MR_CHECK(_r == ncclSuccess, std::string(#call) + ": " + ncclGetErrorString(_r)); \
+  } while (0)
+
+int Engine::set_rccl(const unsigned char* id, int rank, int world) {
+  MR_CHECK(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
+  MR_HIP(hipSetDevice(device));
+  ncclUniqueId uid;
+  static_assert(sizeof(uid.internal) == 128, "ncclUniqueId size");
+  memcpy(uid.internal, id, 128);
+  ncclComm_t c;
+  MR_NCCL(ncclCommInitRank(&c, world, uid, rank));
+  rccl = (void*)c;
+  rccl_world = world;
+  rccl_rank = rank;
+  return 0;
+}
+
+// Sum the CG scalar slot over ranks.  RCCL: in place on the device, ordered on
+// the engine stream (no host synchronisation).  Callbacks: staged via host.
 int Engine::allreduce_state_slot() {
   if (!sharded()) return 0;
+  if (rccl) {
+    MR_NCCL(ncclAllReduce(&d_state->comm[0], &d_state->comm[0], 1, ncclDouble, ncclSum,
+                          (ncclComm_t)rccl, stream));
+    return 0;
+  }
   MR_HIP(hipMemcpyAsync(h_stage, &d_state->comm[0], sizeof(double),
                         hipMemcpyDeviceToHost, stream));
   MR_HIP(hipStreamSynchronize(stream));
@@ -333,8 +363,27 @@ int Engine::allreduce_state_slot() {
   return 0;
 }
 
+// Replicate the freshly solved shard rows of a factor table on every rank.
+// RCCL: all-gather-v as one group of in-place broadcasts, rank r the root of
+// rows [row_begin[r], row_begin[r+1]) (fac rows and, for users, the bias).
 int Engine::allgather_side(bool user) {
   if (!sharded()) return 0;
+  const std::vector<long long>& rb = user ? row_begin_u : row_begin_i;
+  if (rccl) {
+    float* fac = user ? Ufac : Vfac;
+    MR_NCCL(ncclGroupStart());
+    for (int r = 0; r < rccl_world; ++r) {
+      const long long n = rb[r + 1] - rb[r];
+      if (n <= 0) continue;
+      MR_NCCL(ncclBroadcast(fac + rb[r] * ldk, fac + rb[r] * ldk, (size_t)(n * ldk), ncclFloat,
+                            r, (ncclComm_t)rccl, stream));
+      if (user)
+        MR_NCCL(ncclBroadcast(Ubias + rb[r], Ubias + rb[r], (size_t)n, ncclFloat, r,
+                              (ncclComm_t)rccl, stream));
+    }
+    MR_NCCL(ncclGroupEnd());
+    return 0;
+  }
   const int64_t rows = user ? U : I;
   // gather [fac | bias] rows through host staging
   const int64_t rowf = user ? ldk + 1 : ldk;
@@ -349,7 +398,6 @@ int Engine::allgather_side(bool user) {
     memcpy(&tab[r * rowf], &fac[r * ldk], ldk * 4);
     if (user) tab[r * rowf + ldk] = bias[r];
   }
-  const std::vector<long long>& rb = user ? row_begin_u : row_begin_i;
   MR_CHECK(comm.allgather_rows(comm.user, tab.data(), rowf, rb.data(), comm.world) == 0,
            "allgather callback failed");
   for (int64_t r = 0; r < rows; ++r) {

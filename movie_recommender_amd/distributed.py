@@ -106,14 +106,42 @@ class TorchComm:
             return -1
 
 
+def attach_rccl(ctx, rank, world, user_begin, item_begin):
+    """Give ``ctx`` a native RCCL communicator: rank 0 draws the unique id,
+    ``torch.distributed`` (any backend) broadcasts its 128 bytes, then every
+    rank builds the communicator inside the library (collective call)."""
+    import torch.distributed as dist
+    L = _lib.lib()
+    buf = ctypes.create_string_buffer(128)
+    if rank == 0:
+        _lib.check(L.mr_rccl_unique_id(buf), "mr_rccl_unique_id")
+    obj = [bytes(buf.raw) if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(obj, src=0)
+    uid = ctypes.create_string_buffer(obj[0], 128)
+    ub = np.ascontiguousarray(user_begin, dtype=np.int64)
+    ib = np.ascontiguousarray(item_begin, dtype=np.int64)
+    _lib.check(L.mr_als_set_rccl(ctx._h, uid, int(rank), int(world),
+                                 ub.ctypes.data_as(_lib.LLP), ib.ctypes.data_as(_lib.LLP)),
+               "mr_als_set_rccl")
+    ctx._rccl = (ub, ib)
+
+
 def sharded_context(user_ids, item_ids, ratings, k, num_users, num_items, device,
-                    comm, **kw):
-    """Build this rank's ``AlsContext`` and attach ``comm`` (a TorchComm)."""
+                    comm="rccl", **kw):
+    """Build this rank's ``AlsContext`` over an initialised torch.distributed
+    group and attach its collectives: ``comm="rccl"`` (native, device-side),
+    or a ``TorchComm`` (host-staged callbacks; works with gloo)."""
+    import torch.distributed as dist
     from .engine import AlsContext
+    rank, world = dist.get_rank(), dist.get_world_size()
     (u0, u1), (i0, i1), uv, iv, ub, ib = shard_views(
-        user_ids, item_ids, ratings, num_users, num_items, comm.rank, comm.world)
+        user_ids, item_ids, ratings, num_users, num_items, rank, world)
     ctx = AlsContext(uv[0], uv[1], uv[2], k, num_users, num_items, device=device,
                      user_range=(u0, u1), item_range=(i0, i1), item_view=iv, **kw)
-    ctx.set_comm(comm.struct, ub, ib)
-    ctx._comm_owner = comm
+    if comm == "rccl":
+        attach_rccl(ctx, rank, world, ub, ib)
+    else:
+        ctx.set_comm(comm.struct, ub, ib)
+        ctx._comm_owner = comm
     return ctx

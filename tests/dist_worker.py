@@ -1,0 +1,120 @@
+"""Worker for the multi-process tests (launched by torch.distributed.run).
+
+    python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port P tests/dist_worker.py --mode oracle --fixture NAME --out F
+
+Modes
+  oracle       CPU only: the sharded ALS algorithm (rank-local normal
+               equations, all-reduced CG scalars, all-gathered factor shards)
+               restated with the NumPy oracle over gloo; rank 0 saves U, V, ret.
+  engine_gloo  the HIP engine, one shard context per rank (all on cuda:0 when
+               the box has one GPU), collectives through TorchComm callbacks.
+  engine_rccl  the HIP engine with its native RCCL communicator.
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+
+
+def load(name):
+    with np.load(os.path.join(HERE, "golden", name), allow_pickle=False) as d:
+        return {k: d[k] for k in d.files}
+
+
+def oracle_sharded(d, max_iteration, rank, world):
+    """Restatement of the sharded algorithm with the oracle's pieces."""
+    import torch
+    import torch.distributed as dist
+    from oracle import als_oracle as O
+    from movie_recommender_amd.distributed import shard_views
+
+    k = int(d["k"])
+    nU, nI = int(d["num_users"]), int(d["num_items"])
+    u, i, r = d["user_ids"], d["item_ids"], d["ratings"]
+    (u0, u1), (i0, i1), uv, iv, ub, ib = shard_views(u, i, r, nU, nI, rank, world)
+
+    def gdot(a, b):
+        t = torch.tensor([float(np.dot(a, b))], dtype=torch.float64)
+        dist.all_reduce(t)
+        return float(t.item())
+
+    def allgather_rows(table, bounds, width):
+        mine = torch.from_numpy(table[bounds[rank] * width: bounds[rank + 1] * width].copy())
+        sizes = [int(bounds[q + 1] - bounds[q]) * width for q in range(world)]
+        m = max(sizes)
+        send = torch.zeros(m, dtype=torch.float64)
+        send[:len(mine)] = mine
+        outs = [torch.zeros(m, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(outs, send)
+        for q in range(world):
+            table[bounds[q] * width: bounds[q] * width + sizes[q]] = outs[q][:sizes[q]].numpy()
+
+    U = np.array(d["U0"], np.float64)
+    V = np.array(d["V0"], np.float64)
+    it, old_rr = 0, 0.0
+    while it < max_iteration:
+        # user half-step on local users [u0, u1)
+        G, c = O.gram_user(uv[0] - u0, uv[1], uv[2], V, k, u1 - u0)
+        x = U[u0 * (k + 1): u1 * (k + 1)].copy()
+        O.cg_normal(O.block_matvec(G), c.reshape(-1), x, 0.01, 200, dot=gdot)
+        U[u0 * (k + 1): u1 * (k + 1)] = x
+        allgather_rows(U, ub, k + 1)
+        # item half-step on local items [i0, i1)
+        G, c = O.gram_item(iv[0], iv[1] - i0, iv[2], U, k, i1 - i0)
+        x = V[i0 * k: i1 * k].copy()
+        _, rr = O.cg_normal(O.block_matvec(G), c.reshape(-1), x, 0.01, 200, dot=gdot)
+        V[i0 * k: i1 * k] = x
+        allgather_rows(V, ib, k)
+        if it >= 3 and (old_rr - rr) / old_rr < 0.01:
+            return U, V, it
+        old_rr = rr
+        it += 1
+    return U, V, it
+
+
+def engine_sharded(d, max_iteration, rank, world, mode):
+    import torch.distributed as dist
+    from movie_recommender_amd.distributed import TorchComm, sharded_context
+    from movie_recommender_amd.engine import device_count
+    k = int(d["k"])
+    dev = rank % max(1, device_count())
+    comm = "rccl" if mode == "engine_rccl" else TorchComm()
+    ctx = sharded_context(d["user_ids"], d["item_ids"], d["ratings"], k,
+                          int(d["num_users"]), int(d["num_items"]), dev, comm)
+    ctx.set_factors(d["U0"], d["V0"])
+    ret = ctx.run(0.01, max_iteration)
+    U, V = ctx.get_factors()
+    ctx.close()
+    dist.barrier()
+    return U, V, ret
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", required=True)
+    ap.add_argument("--fixture", required=True)
+    ap.add_argument("--max-iteration", type=int, default=200)
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    d = load(a.fixture)
+    if a.mode == "oracle":
+        U, V, ret = oracle_sharded(d, a.max_iteration, rank, world)
+    else:
+        U, V, ret = engine_sharded(d, a.max_iteration, rank, world, a.mode)
+    if rank == 0:
+        np.savez(a.out, U=U, V=V, ret=ret)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
