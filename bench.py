@@ -134,6 +134,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-frac", type=float, default=0.08)
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--force-shard", action="store_true",
+                    help="use the sharded RCCL path even with one rank (testing)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r01.json"),
                     help="per-kernel HBM bytes from a rocprofv3 --pmc run (optional)")
     args = ap.parse_args()
@@ -142,7 +144,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    if world > 1 or args.force_shard:
         import torch
         import torch.distributed as tdist
         torch.cuda.set_device(local_rank)
@@ -166,7 +168,7 @@ def main():
     V0 = rng.uniform(-1, 1, rs.num_items * k)
 
     t0 = time.perf_counter()
-    if world > 1:
+    if dist is not None:
         ctx = sharded_context(rs.user_ids, rs.item_ids, rs.ratings, k, rs.num_users,
                               rs.num_items, local_rank, "rccl", solver=args.solver,
                               ridge=args.ridge)

@@ -225,12 +225,13 @@ int Engine::init(int dev, int k_, int64_t U_, int64_t I_, int64_t n_u,
   su.e0 = u0; su.E = u1 - u0;
   si.e0 = i0; si.E = i1 - i0;
   // factor tables (replicated), zero padding columns
-  if (dalloc(&Ufac, U * ldk, stream) || dalloc(&Ubias, U, stream) ||
-      dalloc(&Vfac, I * ldk, stream))
+  // one extra all-zero row per table: the Gram kernel's padding target
+  if (dalloc(&Ufac, (U + 1) * ldk, stream) || dalloc(&Ubias, U + 1, stream) ||
+      dalloc(&Vfac, (I + 1) * ldk, stream))
     return -1;
-  MR_HIP(hipMemsetAsync(Ufac, 0, std::max<int64_t>(1, U * ldk) * 4, stream));
-  MR_HIP(hipMemsetAsync(Ubias, 0, std::max<int64_t>(1, U) * 4, stream));
-  MR_HIP(hipMemsetAsync(Vfac, 0, std::max<int64_t>(1, I * ldk) * 4, stream));
+  MR_HIP(hipMemsetAsync(Ufac, 0, (U + 1) * ldk * 4, stream));
+  MR_HIP(hipMemsetAsync(Ubias, 0, (U + 1) * 4, stream));
+  MR_HIP(hipMemsetAsync(Vfac, 0, (I + 1) * ldk * 4, stream));
   // upload + build both views
   const bool same = (uv_uid == iv_uid && uv_iid == iv_iid && uv_r == iv_r && n_u == n_i);
   for (int view = 0; view < (same ? 1 : 2); ++view) {
@@ -482,7 +483,7 @@ int Engine::gram(Side& S) {
   const int cls = user ? MR_K_GRAM_USERS : MR_K_GRAM_ITEMS;
   if (tic(cls, -1, &a)) return -1;
   if (launch_gram(stream, user, k, S.work, S.n_work, S.idx, S.val, F, bias,
-                  direct_dst(S), slab_dst(S)))
+                  (int)(user ? I : U), direct_dst(S), slab_dst(S)))
     return -1;
   if (toc(cls, -1, a)) return -1;
   if (S.n_split) {

@@ -68,73 +68,87 @@ __device__ __forceinline__ double block_sum_f64(double v, double* sh) {
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 constexpr int GRAM_WAVES = 4;
 
-// Per-lane copy of one 64-rating chunk: opposite id and weight.
+// Per-lane copy of one 64-rating chunk: opposite id, rating and (item side)
+// the opposite bias.  Slots past the end of the work item point at the
+// table's all-zero row `zrow` with rating 0, so gathers and MFMAs need no
+// masks.  The weight w = r - bias is formed only when the chunk becomes
+// current (one chunk after its loads were issued), so no load is waited on
+// early.
+struct ChunkRaw {
+  int idx;
+  float r;
+  float b;
+};
 struct ChunkRegs {
   int idx;
   float w;
 };
 
-template <bool USER>
-__device__ __forceinline__ ChunkRegs load_chunk(const int32_t* __restrict__ idx,
-                                                const float* __restrict__ val,
-                                                const float* __restrict__ bias,
-                                                int64_t begin, int64_t end, int c,
-                                                int lane) {
+// Stage 1 of a chunk: ids and ratings (independent loads).
+__device__ __forceinline__ ChunkRaw load_chunk(const int32_t* __restrict__ idx,
+                                               const float* __restrict__ val,
+                                               int64_t begin, int64_t end, int c,
+                                               int lane, int zrow) {
   const int64_t jj = begin + 64 * (int64_t)c + lane;
   const bool ok = jj < end;
+  const int64_t js = ok ? jj : begin;           // always a valid address
+  ChunkRaw r;
+  const int i0 = idx[js];
+  const float v0 = val[js];
+  r.idx = ok ? i0 : zrow;
+  r.r = ok ? v0 : 0.f;
+  r.b = 0.f;
+  return r;
+}
+
+// Stage 2 (item side): the opposite bias, gathered through the ids loaded
+// one rotation earlier (bias[zrow] == 0).
+template <bool USER>
+__device__ __forceinline__ void load_bias(ChunkRaw& c, const float* __restrict__ bias) {
+  if (!USER) c.b = bias[c.idx];
+}
+
+__device__ __forceinline__ ChunkRegs finish_chunk(const ChunkRaw& c) {
   ChunkRegs r;
-  r.idx = ok ? idx[jj] : -1;
-  r.w = ok ? val[jj] : 0.f;
-  if (!USER) {
-    const float b = bias[ok ? r.idx : 0];
-    r.w = ok ? r.w - b : 0.f;
-  }
+  r.idx = c.idx;
+  r.w = c.r - c.b;
   return r;
 }
 
 // Gather the rows of G steps (4 ratings each) into registers.  Lane l takes
 // row (l>>4) of each step and its NB contiguous floats starting at natural
 // column NB*(l&15): a[u][b] = F[row][NB*(l&15) + b] is the operand of virtual
-// block b.  For NB % 4 == 0 this is NB/4 dwordx4 loads (k = 64: one 1-KiB
-// wave-instruction fetches 4 whole rows).  Padding columns of F (k <= c < ldk)
-// are zero by construction, so only whole segments beyond ldk are masked.
+// block b (k = 64: one dwordx4 per lane, a 1-KiB wave-instruction = 4 whole
+// rows).  Fc is the lane's column base, one v_mad_u64_u32 per row address.
 template <int NB, int G>
 __device__ __forceinline__ void gather_group(float (&a)[G][NB], float (&ww)[G], ChunkRegs cr,
-                                             int step0_in_chunk, int steps_left,
-                                             const float* __restrict__ F, int k, int ldk,
-                                             int q, int col) {
-  const int c0 = NB * col;
+                                             int step0_in_chunk, const char* __restrict__ Fc,
+                                             uint32_t row_bytes, int q) {
 #pragma unroll
   for (int u = 0; u < G; ++u) {
-    const int src = (4 * (step0_in_chunk + u) + q) & 63;
+    const int src = 4 * (step0_in_chunk + u) + q;
     const int ri = __shfl(cr.idx, src, 64);
-    const float wv = __shfl(cr.w, src, 64);
-    const bool ok = (u < steps_left) && (ri >= 0);
-    ww[u] = ok ? wv : 0.f;
-    const int64_t rowb = (int64_t)(ok ? ri : 0) * ldk;
+    ww[u] = __shfl(cr.w, src, 64);
+    const char* p = Fc + (uint64_t)(uint32_t)ri * row_bytes;
     if constexpr (NB % 4 == 0) {
-      const bool okv = ok && (c0 < ldk);
 #pragma unroll
       for (int h = 0; h < NB / 4; ++h) {
-        const float4 v = *reinterpret_cast<const float4*>(F + (okv ? rowb + c0 + 4 * h : 0));
-        a[u][4 * h + 0] = okv ? v.x : 0.f;
-        a[u][4 * h + 1] = okv ? v.y : 0.f;
-        a[u][4 * h + 2] = okv ? v.z : 0.f;
-        a[u][4 * h + 3] = okv ? v.w : 0.f;
+        const float4 v = *reinterpret_cast<const float4*>(p + 16 * h);
+        a[u][4 * h + 0] = v.x;
+        a[u][4 * h + 1] = v.y;
+        a[u][4 * h + 2] = v.z;
+        a[u][4 * h + 3] = v.w;
       }
-    } else if constexpr (NB == 2) {
-      const bool okv = ok && (c0 < ldk);
-      const float2 v = *reinterpret_cast<const float2*>(F + (okv ? rowb + c0 : 0));
-      a[u][0] = okv ? v.x : 0.f;
-      a[u][1] = okv ? v.y : 0.f;
+    } else if constexpr (NB % 2 == 0) {
+#pragma unroll
+      for (int h = 0; h < NB / 2; ++h) {
+        const float2 v = *reinterpret_cast<const float2*>(p + 8 * h);
+        a[u][2 * h + 0] = v.x;
+        a[u][2 * h + 1] = v.y;
+      }
     } else {
 #pragma unroll
-      for (int b = 0; b < NB; ++b) {
-        const int c = c0 + b;
-        const bool okc = ok && (c < k);
-        const float v = F[okc ? rowb + c : 0];
-        a[u][b] = okc ? v : 0.f;
-      }
+      for (int b = 0; b < NB; ++b) a[u][b] = *reinterpret_cast<const float*>(p + 4 * b);
     }
   }
 }
@@ -146,7 +160,7 @@ __device__ __forceinline__ void mfma_group(floatx4 (&acc)[NB * (NB + 1) / 2],
                                            int steps_left) {
 #pragma unroll
   for (int u = 0; u < G; ++u) {
-    if (u < steps_left) {
+    if (u < steps_left) {     // wave-uniform (scalar) test
       int t = 0;
 #pragma unroll
       for (int bi = 0; bi < NB; ++bi)
@@ -165,24 +179,29 @@ __device__ __forceinline__ void mfma_group(floatx4 (&acc)[NB * (NB + 1) / 2],
   }
 }
 
-template <int NB, int G, bool USER>
+template <int NB, int G, bool USER, bool NTS>
 __global__ __launch_bounds__(256) void gram_kernel(
     const WorkItem* __restrict__ work, int64_t n_work,
     const int32_t* __restrict__ idx, const float* __restrict__ val,
-    const float* __restrict__ F, const float* __restrict__ bias, int k, int ldk,
+    const float* __restrict__ F, const float* __restrict__ bias, int k, int ldk, int zrow,
     GramDst direct, GramDst slab) {
   constexpr int T = NB * (NB + 1) / 2;
   constexpr int GPC = 16 / G;              // groups per 64-rating chunk
   const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t wi = (int64_t)blockIdx.x * GRAM_WAVES + wid;
   if (wi >= n_work) return;  // waves are independent: no block barriers below
-  const WorkItem w = work[wi];
+  // work-item fields in SGPRs: all control flow below is scalar
+  const int64_t wbeg = work[wi].begin;
+  const int wlen = work[wi].len;
+  const int went = work[wi].entity;
+  const int wslab = work[wi].slab;
   const int q = lane >> 4, col = lane & 15;
-  const int64_t end = w.begin + w.len;
-  const int nst = (w.len + 3) >> 2;              // steps of 4 ratings
+  const int64_t end = wbeg + wlen;
+  const int nst = (wlen + 3) >> 2;              // steps of 4 ratings
   const int ngroups = (nst + G - 1) / G;
-  const int nchunks = (w.len + 63) >> 6;
+  const uint32_t row_bytes = (uint32_t)ldk * 4u;
+  const char* Fc = reinterpret_cast<const char*>(F) + 4 * NB * col;
 
   floatx4 acc[T];
 #pragma unroll
@@ -192,31 +211,36 @@ __global__ __launch_bounds__(256) void gram_kernel(
   for (int b = 0; b < NB; ++b) { cacc[b] = 0.f; sacc[b] = 0.f; }
   float wsum = 0.f;
 
-  // software pipeline: buffers A/B hold the gathered rows of two groups;
-  // chunk registers cur (chunk cc) / nxt (chunk cc+1) feed the gathers.
+  // Software pipeline over groups of G steps: while group g's MFMAs run,
+  // the rows of group g+1 are in flight (buffers A/B alternate).  Every
+  // gather is unconditional (slots past the end read the zero row), so the
+  // loads land directly in the buffer registers without merge copies; only
+  // the chunk registers rotate, once per 64 ratings, under a scalar branch.
+  // chunk pipeline: cur (in use), nxt (ids, ratings and bias loaded), nx2
+  // (ids and ratings loaded; its bias gather is issued at the next rotation)
   float aA[G][NB], wA[G], aB[G][NB], wB[G];
-  int cc = 0;
-  ChunkRegs cur = load_chunk<USER>(idx, val, bias, w.begin, end, 0, lane);
-  ChunkRegs nxt = load_chunk<USER>(idx, val, bias, w.begin, end, 1, lane);
-  auto issue = [&](float (&a)[G][NB], float (&ww)[G], int g) {
-    const int ch = g / GPC;
-    if (ch == cc + 2) {   // rotate the chunk registers (wave-uniform)
-      cur = nxt;
-      nxt = load_chunk<USER>(idx, val, bias, w.begin, end, cc + 2, lane);
-      ++cc;
-    }
-    const ChunkRegs cr = (ch == cc) ? cur : nxt;
-    gather_group<NB, G>(a, ww, cr, (g % GPC) * G, nst - g * G, F, k, ldk, q, col);
+  ChunkRaw c0 = load_chunk(idx, val, wbeg, end, 0, lane, zrow);
+  ChunkRaw nxt = load_chunk(idx, val, wbeg, end, 1, lane, zrow);
+  ChunkRaw nx2 = load_chunk(idx, val, wbeg, end, 2, lane, zrow);
+  load_bias<USER>(c0, bias);
+  load_bias<USER>(nxt, bias);
+  ChunkRegs cur = finish_chunk(c0);
+  int nchunk = 3;   // index of the next chunk to load
+  auto rotate = [&]() {
+    cur = finish_chunk(nxt);
+    nxt = nx2;
+    load_bias<USER>(nxt, bias);
+    nx2 = load_chunk(idx, val, wbeg, end, nchunk++, lane, zrow);
   };
-  if (ngroups > 0) issue(aA, wA, 0);
+  gather_group<NB, G>(aA, wA, cur, 0, Fc, row_bytes, q);
   for (int g = 0; g < ngroups; g += 2) {
-    if (g + 1 < ngroups) issue(aB, wB, g + 1);
+    if ((g + 1) % GPC == 0) rotate();
+    gather_group<NB, G>(aB, wB, cur, ((g + 1) % GPC) * G, Fc, row_bytes, q);
     mfma_group<NB, G, USER>(acc, cacc, sacc, wsum, aA, wA, nst - g * G);
-    if (g + 2 < ngroups) issue(aA, wA, g + 2);
-    if (g + 1 < ngroups)
-      mfma_group<NB, G, USER>(acc, cacc, sacc, wsum, aB, wB, nst - (g + 1) * G);
+    if ((g + 2) % GPC == 0) rotate();
+    gather_group<NB, G>(aA, wA, cur, ((g + 2) % GPC) * G, Fc, row_bytes, q);
+    mfma_group<NB, G, USER>(acc, cacc, sacc, wsum, aB, wB, nst - (g + 1) * G);
   }
-  (void)nchunks;
 
   // ---- epilogue -----------------------------------------------------------
 #pragma unroll
@@ -228,19 +252,17 @@ __global__ __launch_bounds__(256) void gram_kernel(
       sacc[b] += __shfl_xor(sacc[b], 32, 64);
     }
   }
-  const bool to_slab = w.slab >= 0;
-  const int64_t di = to_slab ? (int64_t)w.slab : (int64_t)w.entity;
+  const bool to_slab = wslab >= 0;
+  const int64_t di = to_slab ? (int64_t)wslab : (int64_t)went;
   const GramDst& D = to_slab ? slab : direct;
   float* __restrict__ Gd = D.G + di * D.sG;
   float* __restrict__ Cd = D.C + di * D.sV;
   if (q == 0) {
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      const int c = NB * col + b;   // natural column of virtual (b, col)
-      if (c < ldk) {
-        Cd[c] = (c < k) ? cacc[b] : 0.f;
-        if (USER) D.Gs[di * D.sV + c] = (c < k) ? sacc[b] : 0.f;
-      }
+      const int c = NB * col + b;   // natural column of virtual (b, col); c < ldk
+      Cd[c] = (c < k) ? cacc[b] : 0.f;
+      if (USER) D.Gs[di * D.sV + c] = (c < k) ? sacc[b] : 0.f;
     }
   }
   if (USER) {
@@ -248,26 +270,39 @@ __global__ __launch_bounds__(256) void gram_kernel(
                      (__shfl(wsum, 32, 64) + __shfl(wsum, 48, 64));
     if (lane == 0) {
       D.Cb[di * D.sS] = wt;
-      D.Gn[di * D.sS] = (float)w.len;
+      D.Gn[di * D.sS] = (float)wlen;
     }
   }
 #pragma unroll
   for (int t = 0; t < T; ++t)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) Gd[t * 256 + (4 * q + r) * 16 + col] = acc[t][r];
+    for (int r = 0; r < 4; ++r) {
+      float* dst = &Gd[t * 256 + (4 * q + r) * 16 + col];
+      if constexpr (NTS) __builtin_nontemporal_store(acc[t][r], dst);
+      else *dst = acc[t][r];
+    }
 }
 
 template <int NB, int G>
 static int launch_gram_g(hipStream_t s, bool user_side, int k, const WorkItem* work,
                          int64_t n_work, const int32_t* idx, const float* val,
-                         const float* F, const float* bias, GramDst direct, GramDst slab) {
+                         const float* F, const float* bias, int zrow, GramDst direct,
+                         GramDst slab) {
   const int64_t grid = (n_work + GRAM_WAVES - 1) / GRAM_WAVES;
-  if (user_side)
-    gram_kernel<NB, G, true><<<dim3((unsigned)grid), dim3(256), 0, s>>>(
-        work, n_work, idx, val, F, bias, k, ldk_of(k), direct, slab);
-  else
-    gram_kernel<NB, G, false><<<dim3((unsigned)grid), dim3(256), 0, s>>>(
-        work, n_work, idx, val, F, bias, k, ldk_of(k), direct, slab);
+  static int nts = -1;
+  if (nts < 0) {
+    const char* e = getenv("MR_GRAM_NT_STORE");
+    nts = (e && atoi(e) == 1) ? 1 : 0;
+  }
+#define MR_GRAM_LAUNCH(U, N)                                                  \
+  gram_kernel<NB, G, U, N><<<dim3((unsigned)grid), dim3(256), 0, s>>>(        \
+      work, n_work, idx, val, F, bias, k, ldk_of(k), zrow, direct, slab)
+  if (user_side) {
+    if (nts) MR_GRAM_LAUNCH(true, true); else MR_GRAM_LAUNCH(true, false);
+  } else {
+    if (nts) MR_GRAM_LAUNCH(false, true); else MR_GRAM_LAUNCH(false, false);
+  }
+#undef MR_GRAM_LAUNCH
   MR_HIP(hipGetLastError());
   return 0;
 }
@@ -288,21 +323,22 @@ static int gram_group_size(int nb) {
 template <int NB>
 static int launch_gram_nb(hipStream_t s, bool user_side, int k, const WorkItem* work,
                           int64_t n_work, const int32_t* idx, const float* val,
-                          const float* F, const float* bias, GramDst direct, GramDst slab) {
+                          const float* F, const float* bias, int zrow, GramDst direct,
+                          GramDst slab) {
   if (n_work <= 0) return 0;
   switch (gram_group_size(NB)) {
-    case 2: return launch_gram_g<NB, 2>(s, user_side, k, work, n_work, idx, val, F, bias, direct, slab);
-    case 4: return launch_gram_g<NB, 4>(s, user_side, k, work, n_work, idx, val, F, bias, direct, slab);
-    default: return launch_gram_g<NB, 8>(s, user_side, k, work, n_work, idx, val, F, bias, direct, slab);
+    case 2: return launch_gram_g<NB, 2>(s, user_side, k, work, n_work, idx, val, F, bias, zrow, direct, slab);
+    case 4: return launch_gram_g<NB, 4>(s, user_side, k, work, n_work, idx, val, F, bias, zrow, direct, slab);
+    default: return launch_gram_g<NB, 8>(s, user_side, k, work, n_work, idx, val, F, bias, zrow, direct, slab);
   }
 }
 
 int launch_gram(hipStream_t s, bool user_side, int k, const WorkItem* work,
                 int64_t n_work, const int32_t* idx, const float* val,
-                const float* F, const float* bias, GramDst direct,
+                const float* F, const float* bias, int zrow, GramDst direct,
                 GramDst slab) {
 #define MR_GRAM_CASE(NB) \
-  case NB: return launch_gram_nb<NB>(s, user_side, k, work, n_work, idx, val, F, bias, direct, slab);
+  case NB: return launch_gram_nb<NB>(s, user_side, k, work, n_work, idx, val, F, bias, zrow, direct, slab);
   switch (nb16_of(k)) {
     MR_GRAM_CASE(1) MR_GRAM_CASE(2) MR_GRAM_CASE(3) MR_GRAM_CASE(4)
     MR_GRAM_CASE(5) MR_GRAM_CASE(6) MR_GRAM_CASE(7) MR_GRAM_CASE(8)
@@ -389,7 +425,7 @@ int launch_slab_reduce(hipStream_t s, bool user_side, int k,
 // ---------------------------------------------------------------------------
 constexpr int MV_WAVES = 4;
 
-template <int NB, bool USER>
+template <int NB, bool USER, bool NT>
 __global__ __launch_bounds__(256) void cg_matvec_kernel(
     const CgState* __restrict__ st, int update_p, int64_t E, int k, int ldk,
     const float* __restrict__ G, const float* __restrict__ Gs,
@@ -410,25 +446,49 @@ __global__ __launch_bounds__(256) void cg_matvec_kernel(
   double dsum = 0.0;
   for (int64_t e = (int64_t)blockIdx.x * MV_WAVES + wid; e < E;
        e += (int64_t)gridDim.x * MV_WAVES) {
+    // issue order matters for the in-order vmcnt: vector loads first, then
+    // every G block of this entity, so staging p waits only for the former
+    constexpr int NV = (NP + 63) / 64;
     float* ve = v + e * ldk;
-    for (int i = lane; i < NP; i += 64) {   // i: natural index; stored virtual
-      float vi = 0.f;
-      if (i < ldk) {
-        vi = ve[i];
-        if (update_p) {
-          vi = fmaf(beta, vi, -r[e * ldk + i]);
-          ve[i] = vi;
-        }
-      }
-      pv[wid][virt_of(i, NB)] = vi;
+    float vi[NV], ri[NV];
+#pragma unroll
+    for (int h = 0; h < NV; ++h) {
+      const int i = lane + 64 * h;
+      vi[h] = (i < NP) ? ve[i] : 0.f;                       // NP == ldk
+      ri[h] = (update_p && i < NP) ? r[e * ldk + i] : 0.f;
     }
-    float vbias = 0.f;
+    float vbias = 0.f, rbias = 0.f;
     if (USER) {
       vbias = vb[e];
-      if (update_p) {
-        vbias = fmaf(beta, vbias, -rb[e]);
-        if (lane == 0) vb[e] = vbias;
+      if (update_p) rbias = rb[e];
+    }
+    const float4* __restrict__ Ge = reinterpret_cast<const float4*>(G + e * (int64_t)T * 256);
+    float4 g[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      if constexpr (NT) {
+        const floatx4 x = __builtin_nontemporal_load(
+            reinterpret_cast<const floatx4*>(Ge) + t * 64 + lane);
+        g[t] = make_float4(x[0], x[1], x[2], x[3]);
+      } else {
+        g[t] = Ge[t * 64 + lane];
       }
+    }
+#pragma unroll
+    for (int h = 0; h < NV; ++h) {
+      const int i = lane + 64 * h;
+      if (i < NP) {
+        float x = vi[h];
+        if (update_p) {
+          x = fmaf(beta, x, -ri[h]);
+          ve[i] = x;
+        }
+        pv[wid][virt_of(i, NB)] = x;
+      }
+    }
+    if (USER && update_p) {
+      vbias = fmaf(beta, vbias, -rbias);
+      if (lane == 0) vb[e] = vbias;
     }
     __builtin_amdgcn_wave_barrier();
     float accR[NB];
@@ -438,26 +498,25 @@ __global__ __launch_bounds__(256) void cg_matvec_kernel(
       accR[b] = 0.f;
       accC[b] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    const float4* __restrict__ Ge = reinterpret_cast<const float4*>(G + e * (int64_t)T * 256);
     int t = 0;
 #pragma unroll
     for (int bi = 0; bi < NB; ++bi) {
       const float pi = pv[wid][16 * bi + rr];
 #pragma unroll
       for (int bj = bi; bj < NB; ++bj) {
-        const float4 g = Ge[t * 64 + lane];
+        const float4 gg = g[t];
         const float4 pj = *reinterpret_cast<const float4*>(&pv[wid][16 * bj + c4]);
         float s0 = accR[bi];
-        s0 = fmaf(g.x, pj.x, s0);
-        s0 = fmaf(g.y, pj.y, s0);
-        s0 = fmaf(g.z, pj.z, s0);
-        s0 = fmaf(g.w, pj.w, s0);
+        s0 = fmaf(gg.x, pj.x, s0);
+        s0 = fmaf(gg.y, pj.y, s0);
+        s0 = fmaf(gg.z, pj.z, s0);
+        s0 = fmaf(gg.w, pj.w, s0);
         accR[bi] = s0;
         if (bi != bj) {
-          accC[bj].x = fmaf(g.x, pi, accC[bj].x);
-          accC[bj].y = fmaf(g.y, pi, accC[bj].y);
-          accC[bj].z = fmaf(g.z, pi, accC[bj].z);
-          accC[bj].w = fmaf(g.w, pi, accC[bj].w);
+          accC[bj].x = fmaf(gg.x, pi, accC[bj].x);
+          accC[bj].y = fmaf(gg.y, pi, accC[bj].y);
+          accC[bj].z = fmaf(gg.z, pi, accC[bj].z);
+          accC[bj].w = fmaf(gg.w, pi, accC[bj].w);
         }
         ++t;
       }
@@ -504,18 +563,35 @@ __global__ __launch_bounds__(256) void cg_matvec_kernel(
   if (threadIdx.x == 0) partials[blockIdx.x] = tot;
 }
 
+// G streams once per CG iteration and exceeds the Infinity Cache at scale,
+// so it is loaded non-temporally: measured on MI355X (k = 64, ML-full shape)
+// users 225 -> 195 us, items 103 -> 94 us, and the CG update kernel 28 -> 25 us
+// because its vectors stay cached.  MR_MATVEC_NT=0 restores plain loads.
+static bool matvec_nt() {
+  static int env = -1;
+  if (env < 0) {
+    const char* e = getenv("MR_MATVEC_NT");
+    env = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return env == 1;
+}
+
 template <int NB>
 static int launch_matvec_nb(hipStream_t s, bool user_side, const CgState* st, int update_p,
                             int64_t E, int k, const float* G, const float* Gs,
                             const float* Gn, float* v, float* vb, const float* r,
                             const float* rb, float* y, float* yb, double* partials,
                             int n_part) {
-  if (user_side)
-    cg_matvec_kernel<NB, true><<<dim3(n_part), dim3(256), 0, s>>>(
-        st, update_p, E, k, ldk_of(k), G, Gs, Gn, v, vb, r, rb, y, yb, partials);
-  else
-    cg_matvec_kernel<NB, false><<<dim3(n_part), dim3(256), 0, s>>>(
-        st, update_p, E, k, ldk_of(k), G, Gs, Gn, v, vb, r, rb, y, yb, partials);
+  const bool nt = matvec_nt();
+#define MR_MV_LAUNCH(U, N)                                                          \
+  cg_matvec_kernel<NB, U, N><<<dim3(n_part), dim3(256), 0, s>>>(                    \
+      st, update_p, E, k, ldk_of(k), G, Gs, Gn, v, vb, r, rb, y, yb, partials)
+  if (user_side) {
+    if (nt) MR_MV_LAUNCH(true, true); else MR_MV_LAUNCH(true, false);
+  } else {
+    if (nt) MR_MV_LAUNCH(false, true); else MR_MV_LAUNCH(false, false);
+  }
+#undef MR_MV_LAUNCH
   MR_HIP(hipGetLastError());
   return 0;
 }

@@ -30,7 +30,10 @@ const char* last_error();
   } while (0)
 
 constexpr int kMaxK = 128;        // largest factor count the Gram kernel tiles
-inline int ldk_of(int k) { return (k + 3) & ~3; }   // row stride, 16-B rows
+// Row stride of factor tables / CG vectors: k rounded up to a multiple of 16
+// (one packed16 block width), so every Gram lane's NB-float segment of a row
+// lies inside the row; padding columns are kept at zero.
+__host__ __device__ inline int ldk_of(int k) { return (k + 15) & ~15; }
 
 // Normal-equation storage ("packed16"): the k x k block G_e (in the virtual
 // index order below) is cut into 16 x 16 blocks and only the upper-triangular
@@ -122,9 +125,11 @@ enum CgCtl { CTL_REDUCE = 1, CTL_FINALIZE = 2, CTL_BOTH = 3 };
 enum CgUpd { UPD_INIT = 0, UPD_STEP = 1 };
 
 // Kernel launchers (kernels.hip) ---------------------------------------------
+// F has zrow+1 rows; row zrow (and bias[zrow]) is all zero.
 int launch_gram(hipStream_t s, bool user_side, int k, const WorkItem* work,
                 int64_t n_work, const int32_t* idx, const float* val,
-                const float* F, const float* bias, GramDst direct, GramDst slab);
+                const float* F, const float* bias, int zrow, GramDst direct,
+                GramDst slab);
 int launch_slab_reduce(hipStream_t s, bool user_side, int k,
                        const SplitItem* split, int64_t n_split,
                        const float* slab, int64_t rec, GramDst direct);

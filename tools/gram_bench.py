@@ -12,6 +12,7 @@ ap.add_argument("--k", type=int, default=64)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--shape", default="ml-full")
 ap.add_argument("--chunk", type=int, default=None)
+ap.add_argument("--cg", type=int, default=0, help="also run this many ALS iterations")
 a = ap.parse_args()
 cache = f"/tmp/mr_bench_{a.shape}_k{a.k}_{synth.DATA_SEED}.npz"
 if os.path.exists(cache):
@@ -43,4 +44,12 @@ with AlsContext(rs.user_ids, rs.item_ids, rs.ratings, k, rs.num_users, rs.num_it
         nb = (k + 15) // 16
         out[side + "_mfmaTF"] = round(N * nb * (nb + 1) / 2 * 512 / (ms * 1e-3) / 1e12, 1)
     out["slab_ms"] = round(st["kernel_ms"]["slab_reduce"] / max(1, st["kernel_launches"]["slab_reduce"]), 4)
+    if a.cg:
+        ctx.reset_stats()
+        ctx.iterate(a.cg)
+        st = ctx.stats()
+        for c in ("matvec_users", "matvec_items", "cg_update", "cg_control"):
+            n = max(1, st["kernel_launches"][c])
+            out[c + "_us"] = round(st["kernel_ms"][c] / n * 1e3, 2)
+        out["cg_its"] = (st["cg_users_total"], st["cg_items_total"])
     print(json.dumps(out), flush=True)
