@@ -16,10 +16,10 @@ import os
 import re
 
 CLASSES = [
-    ("gram_users", r"gram_kernel<\d+, \d+, true>"),
-    ("gram_items", r"gram_kernel<\d+, \d+, false>"),
-    ("matvec_users", r"cg_matvec_kernel<\d+, true>"),
-    ("matvec_items", r"cg_matvec_kernel<\d+, false>"),
+    ("gram_users", r"gram_kernel<\d+, \d+, true"),
+    ("gram_items", r"gram_kernel<\d+, \d+, false"),
+    ("matvec_users", r"cg_matvec_kernel<\d+, true"),
+    ("matvec_items", r"cg_matvec_kernel<\d+, false"),
     ("slab_reduce", r"slab_reduce_kernel"),
     ("cg_update", r"cg_update_kernel"),
     ("cg_control", r"cg_control_kernel"),
