@@ -57,14 +57,17 @@ def load_data(shape, k, cache_dir="/tmp"):
 def algorithmic_cost(cls, k, n_users, n_items, n_ratings, ldk):
     """(bytes, flops) per launch of a kernel class; definitions in DESIGN.md.
 
-    Normal equations are stored as upper-triangular 16x16 blocks ("packed16":
-    nbp = nb(nb+1)/2 blocks of 256 floats, nb = ceil(k/16)); the CG matvec's
-    bytes are that storage plus the CG vectors it streams.  Gram flops are the
-    full K x K outer products of SURVEY.md 8(d) F(k) (the kernel computes only
-    the upper blocks, so its MFMA work is nbp*512 flop per rating)."""
+    Normal equations are stored "tri16" (mr_internal.h): the nb(nb-1)/2
+    strictly-upper 16x16 blocks, the nb diagonal blocks folded pairwise into
+    nb/2 tiles (+1 full tile for odd nb) and a 16-float diagonal side array
+    per fold, nb = ceil(k/16) -- 2080 floats at k = 64 (k(k+1)/2 = 2080).  The
+    CG matvec's bytes are that storage plus the CG vectors it streams.  Gram
+    flops are the full K x K outer products of SURVEY.md 8(d) F(k) (the kernel
+    computes only the upper blocks, so its MFMA work is nb(nb+1)/2*512 flop
+    per rating)."""
     K = k + 1
     nb = (k + 15) // 16
-    gsz = nb * (nb + 1) // 2 * 256
+    gsz = (nb * (nb - 1) // 2 + nb // 2 + nb % 2) * 256 + (nb // 2) * 16
     if cls == "matvec_users":
         E = n_users
         g = E * (gsz + ldk + 1) * 4               # G_e blocks + Gs row + count

@@ -9,7 +9,9 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <new>
+#include <vector>
 
 #include "../../include/cpp_ls_lib.h"
 #include "engine.h"
@@ -90,10 +92,43 @@ int als_from_python(int* user_ids, int* item_ids, int ratings_length,
     if (eng.init(env_device(), k, U, I, ratings_length, user_ids, item_ids, ratings_values,
                  ratings_length, user_ids, item_ids, ratings_values, 0, U, 0, I))
       return -1;
+    // The reference's loop body never runs for max_iteration <= 0 and the
+    // factors come back untouched (matrix.cpp:814); keep them bit-exact
+    // instead of round-tripping through the fp32 device tables.
+    if (max_iteration <= 0) return 0;
     if (eng.set_factors(user_factors_values, item_factors_values)) return -1;
     const int ret = eng.run(min_r_decrease, max_iteration);
     if (ret < 0) return -1;
+    // Entities without ratings have all-zero normal equations: the reference
+    // CG leaves their x exactly as given (r = p = 0 there).  Restore those
+    // rows in fp64 so they, too, are bit-identical.
+    std::vector<char> seen_u(U, 0), seen_i(I, 0);
+    for (int n = 0; n < ratings_length; ++n) {
+      seen_u[user_ids[n]] = 1;
+      seen_i[item_ids[n]] = 1;
+    }
+    std::vector<double> u_keep, i_keep;
+    for (int u = 0; u < U; ++u)
+      if (!seen_u[u])
+        u_keep.insert(u_keep.end(), user_factors_values + (int64_t)u * (k + 1),
+                      user_factors_values + (int64_t)(u + 1) * (k + 1));
+    for (int i = 0; i < I; ++i)
+      if (!seen_i[i])
+        i_keep.insert(i_keep.end(), item_factors_values + (int64_t)i * k,
+                      item_factors_values + (int64_t)(i + 1) * k);
     if (eng.get_factors(user_factors_values, item_factors_values)) return -1;
+    size_t pu = 0, pi = 0;
+    for (int u = 0; u < U; ++u)
+      if (!seen_u[u]) {
+        std::copy(u_keep.begin() + pu, u_keep.begin() + pu + k + 1,
+                  user_factors_values + (int64_t)u * (k + 1));
+        pu += k + 1;
+      }
+    for (int i = 0; i < I; ++i)
+      if (!seen_i[i]) {
+        std::copy(i_keep.begin() + pi, i_keep.begin() + pi + k, item_factors_values + (int64_t)i * k);
+        pi += k;
+      }
     return ret;
   });
 }

@@ -559,10 +559,16 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr) {
     return control(CG_BETA, seq_of.back());
   };
 
+  // Iteration 0 cannot stop by stagnation (fails starts at 0) and iteration 1
+  // only after two stagnating steps, so both are enqueued behind the init
+  // without waiting for its state (they are no-ops if the init already
+  // finished the solve: rr < 1e-6 or max_it == 0).
+  int launched = 0;          // iterations enqueued so far
+  for (; launched < std::min(2, max_it); ++launched)
+    if (launch_iter(launched)) return -1;
   CgMirror ms{};
   if (wait_mirror(seq_init, &ms)) return -1;
   int known = -1;            // index of the last iteration whose state is in ms
-  int launched = 0;          // iterations enqueued so far
   while (!ms.done) {
     if (launched <= known + 1) {
       if (launch_iter(launched)) return -1;

@@ -59,7 +59,8 @@ __device__ __forceinline__ double block_sum_f64(double v, double* sh) {
 // (bi, bj): D += A_bi^T A_bj over 4 ratings per MFMA.  Only the NB(NB+1)/2
 // upper blocks are computed (k = 64: 10 of 16), and the accumulators are
 // stored as they stand: D[row = 4(l>>4) + reg][col = l&15] is exactly the
-// packed16 block layout, so the epilogue needs no transpose.  The rhs and
+// row-major tile layout of tri16 storage, so the epilogue needs no transpose
+// (diagonal blocks are masked into their folded tile / side array).  The rhs and
 // (user side) row sums / counts ride along on VALU.  Item side:
 // w = r - U[u][k] (fill_ratings_minus_bias, :1021-1030).
 // Rows of UNR steps are gathered before their MFMAs (UNR*NB loads in flight
@@ -273,14 +274,37 @@ __global__ __launch_bounds__(256) void gram_kernel(
       D.Gn[di * D.sS] = (float)wlen;
     }
   }
+  // tri16 layout (mr_internal.h): off-diagonal blocks as full tiles, diagonal
+  // blocks folded pairwise; every store index is compile-time except the lane
+  constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2, NTILE = NO + NF + (NB & 1);
+  auto st = [&](int off, float v) {
+    float* dst = &Gd[off];
+    if constexpr (NTS) __builtin_nontemporal_store(v, dst);
+    else *dst = v;
+  };
+  int t = 0;
 #pragma unroll
-  for (int t = 0; t < T; ++t)
+  for (int bi = 0; bi < NB; ++bi) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float* dst = &Gd[t * 256 + (4 * q + r) * 16 + col];
-      if constexpr (NTS) __builtin_nontemporal_store(acc[t][r], dst);
-      else *dst = acc[t][r];
+    for (int bj = bi; bj < NB; ++bj) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 4 * q + r;
+        const float v = acc[t][r];
+        if (bi != bj) {
+          st(off_index(bi, bj, NB) * 256 + row * 16 + col, v);
+        } else if ((NB & 1) && bi == NB - 1) {
+          st((NO + NF) * 256 + row * 16 + col, v);
+        } else if ((bi & 1) == 0) {
+          if (col >= row) st((NO + (bi >> 1)) * 256 + row * 16 + col, v);
+        } else {
+          if (col < row) st((NO + (bi >> 1)) * 256 + row * 16 + col, v);
+          else if (col == row) st(NTILE * 256 + (bi >> 1) * 16 + row, v);
+        }
+      }
+      ++t;
     }
+  }
 }
 
 template <int NB, int G>
@@ -349,7 +373,7 @@ int launch_gram(hipStream_t s, bool user_side, int k, const WorkItem* work,
 
 // ---------------------------------------------------------------------------
 // Combine partial records of split entities, in slab order (deterministic).
-// Record layout: [gsize G (packed16)][ldk Gs][ldk C][Cb][Gn] (+pad).
+// Record layout: [gsize G (tri16)][ldk Gs][ldk C][Cb][Gn] (+pad).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void store_rec(const GramDst& d, int64_t e, int64_t t, float v,
                                           int64_t nG, int ldk, bool user) {
@@ -413,7 +437,7 @@ int launch_slab_reduce(hipStream_t s, bool user_side, int k,
 }
 
 // ---------------------------------------------------------------------------
-// K2: batched block GEMV y_e = G_e v_e on packed16 storage (+ bias row/col on
+// K2: batched block GEMV y_e = G_e v_e on tri16 storage (+ bias row/col on
 // the user side), with the CG direction update v = -r + beta v fused in front
 // (matrix.cpp:521 of the previous iteration) and the v.y partial dot behind
 // (:497).  One wave per entity, grid-stride with a fixed grid so partial sums
@@ -433,12 +457,14 @@ __global__ __launch_bounds__(256) void cg_matvec_kernel(
     const float* __restrict__ r, const float* __restrict__ rb,
     float* __restrict__ y, float* __restrict__ yb, double* __restrict__ partials) {
   if (st->done) return;
-  constexpr int T = NB * (NB + 1) / 2;
+  constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2, NTILE = NO + NF + (NB & 1);
+  constexpr int64_t GS = (int64_t)NTILE * 256 + NF * 16;   // == gsize_of(k)
   constexpr int NP = 16 * NB;
   constexpr int CST = 68;   // float4 stride of a column-partial row (+16 floats: no bank clash)
   __shared__ float pv[MV_WAVES][NP];
   __shared__ float redR[MV_WAVES][NB][64];
   __shared__ float4 redC[MV_WAVES][NB][CST];
+  __shared__ float dd[MV_WAVES][NF > 0 ? 16 * NF : 1];
   __shared__ double sh[MV_WAVES];
   const float beta = (float)st->beta;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -462,10 +488,10 @@ __global__ __launch_bounds__(256) void cg_matvec_kernel(
       vbias = vb[e];
       if (update_p) rbias = rb[e];
     }
-    const float4* __restrict__ Ge = reinterpret_cast<const float4*>(G + e * (int64_t)T * 256);
-    float4 g[T];
+    const float4* __restrict__ Ge = reinterpret_cast<const float4*>(G + e * GS);
+    float4 g[NTILE];
 #pragma unroll
-    for (int t = 0; t < T; ++t) {
+    for (int t = 0; t < NTILE; ++t) {
       if constexpr (NT) {
         const floatx4 x = __builtin_nontemporal_load(
             reinterpret_cast<const floatx4*>(Ge) + t * 64 + lane);
@@ -474,6 +500,8 @@ __global__ __launch_bounds__(256) void cg_matvec_kernel(
         g[t] = Ge[t * 64 + lane];
       }
     }
+    float d2 = 0.f;   // diagonal of the odd diagonal blocks (side array)
+    if (NF > 0 && lane < 16 * NF) d2 = G[e * GS + NTILE * 256 + lane];
 #pragma unroll
     for (int h = 0; h < NV; ++h) {
       const int i = lane + 64 * h;
@@ -490,6 +518,7 @@ __global__ __launch_bounds__(256) void cg_matvec_kernel(
       vbias = fmaf(beta, vbias, -rbias);
       if (lane == 0) vb[e] = vbias;
     }
+    if (NF > 0 && lane < 16 * NF) dd[wid][lane] = d2;
     __builtin_amdgcn_wave_barrier();
     float accR[NB];
     float4 accC[NB];
@@ -498,12 +527,13 @@ __global__ __launch_bounds__(256) void cg_matvec_kernel(
       accR[b] = 0.f;
       accC[b] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    // strictly-upper tiles: row product into y_bi, column product into y_bj
     int t = 0;
 #pragma unroll
     for (int bi = 0; bi < NB; ++bi) {
       const float pi = pv[wid][16 * bi + rr];
 #pragma unroll
-      for (int bj = bi; bj < NB; ++bj) {
+      for (int bj = bi + 1; bj < NB; ++bj) {
         const float4 gg = g[t];
         const float4 pj = *reinterpret_cast<const float4*>(&pv[wid][16 * bj + c4]);
         float s0 = accR[bi];
@@ -512,14 +542,49 @@ __global__ __launch_bounds__(256) void cg_matvec_kernel(
         s0 = fmaf(gg.z, pj.z, s0);
         s0 = fmaf(gg.w, pj.w, s0);
         accR[bi] = s0;
-        if (bi != bj) {
-          accC[bj].x = fmaf(gg.x, pi, accC[bj].x);
-          accC[bj].y = fmaf(gg.y, pi, accC[bj].y);
-          accC[bj].z = fmaf(gg.z, pi, accC[bj].z);
-          accC[bj].w = fmaf(gg.w, pi, accC[bj].w);
-        }
+        accC[bj].x = fmaf(gg.x, pi, accC[bj].x);
+        accC[bj].y = fmaf(gg.y, pi, accC[bj].y);
+        accC[bj].z = fmaf(gg.z, pi, accC[bj].z);
+        accC[bj].w = fmaf(gg.w, pi, accC[bj].w);
         ++t;
       }
+    }
+    // folded diagonal tiles: c >= r belongs to D_2m (row; column also for
+    // c > r), c < r to D_2m+1 (row and column)
+#pragma unroll
+    for (int m = 0; m < NF; ++m) {
+      const int b0 = 2 * m, b1 = 2 * m + 1;
+      const float4 gg = g[NO + m];
+      const float ge[4] = {gg.x, gg.y, gg.z, gg.w};
+      const float4 p0 = *reinterpret_cast<const float4*>(&pv[wid][16 * b0 + c4]);
+      const float4 p1 = *reinterpret_cast<const float4*>(&pv[wid][16 * b1 + c4]);
+      const float p0c[4] = {p0.x, p0.y, p0.z, p0.w};
+      const float p1c[4] = {p1.x, p1.y, p1.z, p1.w};
+      const float pr0 = pv[wid][16 * b0 + rr], pr1 = pv[wid][16 * b1 + rr];
+      float c0[4], c1[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const int c = c4 + x;
+        const float gu = (c >= rr) ? ge[x] : 0.f;
+        const float gc = (c > rr) ? ge[x] : 0.f;
+        const float gl = (c < rr) ? ge[x] : 0.f;
+        accR[b0] = fmaf(gu, p0c[x], accR[b0]);
+        accR[b1] = fmaf(gl, p1c[x], accR[b1]);
+        c0[x] = gc * pr0;
+        c1[x] = gl * pr1;
+      }
+      accC[b0].x += c0[0]; accC[b0].y += c0[1]; accC[b0].z += c0[2]; accC[b0].w += c0[3];
+      accC[b1].x += c1[0]; accC[b1].y += c1[1]; accC[b1].z += c1[2]; accC[b1].w += c1[3];
+    }
+    if constexpr ((NB & 1) != 0) {   // last diagonal block stored full: row product
+      const float4 gg = g[NO + NF];
+      const float4 pj = *reinterpret_cast<const float4*>(&pv[wid][16 * (NB - 1) + c4]);
+      float s0 = accR[NB - 1];
+      s0 = fmaf(gg.x, pj.x, s0);
+      s0 = fmaf(gg.y, pj.y, s0);
+      s0 = fmaf(gg.z, pj.z, s0);
+      s0 = fmaf(gg.w, pj.w, s0);
+      accR[NB - 1] = s0;
     }
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
@@ -540,6 +605,7 @@ __global__ __launch_bounds__(256) void cg_matvec_kernel(
 #pragma unroll
       for (int qq = 0; qq < 16; ++qq) sc += C[16 * qq];
       yo += sc;
+      if (NF > 0 && (b & 1) && b < 2 * NF) yo = fmaf(dd[wid][(b >> 1) * 16 + ii], pv[wid][o], yo);
       if (USER) {
         const float gs = Gs[e * ldk + n];
         yo = fmaf(gs, vbias, yo);

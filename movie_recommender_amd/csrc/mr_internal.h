@@ -31,32 +31,51 @@ const char* last_error();
 
 constexpr int kMaxK = 128;        // largest factor count the Gram kernel tiles
 // Row stride of factor tables / CG vectors: k rounded up to a multiple of 16
-// (one packed16 block width), so every Gram lane's NB-float segment of a row
+// (one 16-wide block of the tri16 storage), so every Gram lane's NB-float segment of a row
 // lies inside the row; padding columns are kept at zero.
 __host__ __device__ inline int ldk_of(int k) { return (k + 15) & ~15; }
 
-// Normal-equation storage ("packed16"): the k x k block G_e (in the virtual
-// index order below) is cut into 16 x 16 blocks and only the upper-triangular
-// blocks (bi <= bj) are stored, row-major inside each block, blocks in
-// row-major upper order.  Rows/cols >= k are zero.  k = 64: 10 blocks =
-// 2,560 floats instead of 4,096.
+// Normal-equation storage ("tri16").  G_e, over the permuted ("virtual")
+// factor index below, is cut into NB x NB blocks of 16 x 16 (NB = ceil(k/16)):
+//   * the NB(NB-1)/2 strictly-upper blocks (bi < bj) as full tiles, row-major
+//     inside, row-major upper order;
+//   * the diagonal blocks folded in pairs (2m, 2m+1) into ONE tile F_m:
+//     F_m[r][c] = D_2m[r][c] for c >= r, D_2m+1[r][c] for c < r (each D is
+//     bitwise symmetric, so no transpose is ever needed), and the diagonal of
+//     D_2m+1 in a 16-float side array; an odd last diagonal block stays full.
+// k = 64: 8 tiles + 32 floats = 2,080 floats = k(k+1)/2 (full: 4,096).
+// Rows/cols >= k are zero.
 __host__ __device__ inline int nb16_of(int k) { return (k + 15) / 16; }
-__host__ __device__ inline int nbp_of(int k) { return nb16_of(k) * (nb16_of(k) + 1) / 2; }
-__host__ __device__ inline int64_t gsize_of(int k) { return (int64_t)nbp_of(k) * 256; }
-__host__ __device__ inline int blk_index(int bi, int bj, int nb) {
-  return bi * nb - bi * (bi - 1) / 2 + (bj - bi);
+__host__ __device__ inline int n_off_of(int nb) { return nb * (nb - 1) / 2; }
+__host__ __device__ inline int n_fold_of(int nb) { return nb / 2; }
+__host__ __device__ inline int n_tiles_of(int nb) { return n_off_of(nb) + nb / 2 + (nb & 1); }
+__host__ __device__ inline int64_t gsize_of(int k) {
+  const int nb = nb16_of(k);
+  return (int64_t)n_tiles_of(nb) * 256 + n_fold_of(nb) * 16;
+}
+// strictly-upper tile (bi < bj)
+__host__ __device__ inline int off_index(int bi, int bj, int nb) {
+  return bi * nb - bi * (bi + 1) / 2 + (bj - bi - 1);
 }
 // Blocks are formed over a permuted ("virtual") factor index so that every
 // lane of the Gram kernel gathers NB contiguous floats of a row (one dwordx4
 // for k = 64): virtual v = 16*b + i  <->  natural n = NB*i + b.
 __host__ __device__ inline int virt_of(int n, int nb) { return 16 * (n % nb) + n / nb; }
 __host__ __device__ inline int nat_of(int v, int nb) { return nb * (v & 15) + (v >> 4); }
-// Stored element for natural (i, j) of a packed16 G_e, -1 if outside k.
+// Offset of natural element (i, j) of a tri16 G_e.
 __host__ __device__ inline int64_t packed_offset(int i, int j, int nb) {
   int vi = virt_of(i, nb), vj = virt_of(j, nb);
-  if ((vi >> 4) > (vj >> 4)) { const int t = vi; vi = vj; vj = t; }
-  const int bi = vi >> 4, bj = vj >> 4;
-  return (int64_t)blk_index(bi, bj, nb) * 256 + (vi & 15) * 16 + (vj & 15);
+  if ((vi >> 4) > (vj >> 4) || ((vi >> 4) == (vj >> 4) && (vi & 15) > (vj & 15))) {
+    const int t = vi; vi = vj; vj = t;      // symmetric: use (min, max)
+  }
+  const int bi = vi >> 4, bj = vj >> 4, ri = vi & 15, rj = vj & 15;   // ri <= rj if bi == bj
+  if (bi != bj) return (int64_t)off_index(bi, bj, nb) * 256 + ri * 16 + rj;
+  const int base = n_off_of(nb);
+  if ((nb & 1) && bi == nb - 1) return (int64_t)(base + n_fold_of(nb)) * 256 + ri * 16 + rj;
+  const int m = bi >> 1;
+  if ((bi & 1) == 0) return (int64_t)(base + m) * 256 + ri * 16 + rj;       // upper incl. diag
+  if (ri == rj) return (int64_t)n_tiles_of(nb) * 256 + m * 16 + ri;         // side array
+  return (int64_t)(base + m) * 256 + rj * 16 + ri;                          // strict lower
 }
 
 // One wave's unit of Gram work: ratings [begin, begin+len) of one entity's
@@ -78,7 +97,7 @@ struct SplitItem {
 };
 
 // Destination of normal equations: entity / slab i writes
-//   G  + i*sG  (packed16 blocks) Gs + i*sV (sum of rows, user side)
+//   G  + i*sG  (tri16 tiles)     Gs + i*sV (sum of rows, user side)
 //   C  + i*sV  (rhs)            Cb + i*sS (sum of ratings, user side)
 //   Gn + i*sS  (rating count, user side)
 struct GramDst {

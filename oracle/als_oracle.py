@@ -19,6 +19,12 @@ import numpy as np
 import scipy.sparse as sp
 
 
+def _div(a, b):
+    """IEEE-754 division as in the reference's C++ (0/0 -> nan, x/0 -> +-inf)."""
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return float(np.float64(a) / np.float64(b))
+
+
 # --------------------------------------------------------------------------
 # CG on the normal equations  (matrix.cpp:456-529, cg_least_squares)
 # --------------------------------------------------------------------------
@@ -46,12 +52,12 @@ def cg_normal(matvec, c, x, min_r_decrease=0.01, max_iteration=200,
         if rr < 1e-6:
             return it, final_rr
         Ap = matvec(p).astype(vdtype)
-        alpha = rr / dot(p, Ap)
+        alpha = _div(rr, dot(p, Ap))
         x += vdtype(alpha) * p if vdtype is np.float32 else alpha * p
         r += vdtype(alpha) * Ap if vdtype is np.float32 else alpha * Ap
         rr2 = dot(r, r)
         final_rr = rr2
-        beta = rr2 / rr
+        beta = _div(rr2, rr)
         if beta > 1 - min_r_decrease:
             fails += 1
         else:
@@ -142,7 +148,7 @@ def als_design(user_ids, item_ids, ratings, k, U0, V0,
         ci, rr = cg_normal(lambda v: Bt @ (B @ v), Bt @ rb, V, 0.01, 200)  # :854
         trace.append((cu, ci, rr))
         if it >= 3:                                            # :871-875
-            if (old_rr - rr) / old_rr < min_r_decrease:
+            if _div(old_rr - rr, old_rr) < min_r_decrease:
                 return U, V, it, trace
         old_rr = rr
         it += 1
@@ -254,7 +260,7 @@ def als_block(user_ids, item_ids, ratings, k, U0, V0,
         ci, rr = cg_blocks(G, c, V, 0.01, 200)
         trace.append((cu, ci, rr))
         if it >= 3:
-            if (old_rr - rr) / old_rr < min_r_decrease:
+            if _div(old_rr - rr, old_rr) < min_r_decrease:
                 return U.astype(np.float64), V.astype(np.float64), it, trace
         old_rr = rr
         it += 1

@@ -18,6 +18,8 @@ Fixtures
                                  64), max_iteration = 2, 4
   G4  band_ml100k_k10.json       held-out / train RMSE band of the reference
                                  over seeds {0..4} x thread counts {1,2,8}
+  G5  als_edge_*.npz, cg_edge_sparse.npz   max_iteration 0..4, zero ratings,
+                                 duplicate pairs, empty CSR rows / columns
 """
 import json
 import os
@@ -123,6 +125,56 @@ def g3():
             print("G3", name, "N", rs_.n, "ret", ret, "tc spread", spread)
 
 
+def g5():
+    """Edge cases: max_iteration 0..4, zero ratings, duplicate (user, item)
+    pairs, a tiny problem, and a general CG with an empty column/row."""
+    ref.set_thread_count(1)
+    d = dict(np.load(os.path.join(HERE, "als_dense_38x45_k5.npz")))
+    out = {}
+    for mi in range(5):
+        U, V, ret = ref.als(d["user_ids"], d["item_ids"], d["ratings"], 5, d["U0"], d["V0"],
+                            max_iteration=mi)
+        out[f"U_{mi}"], out[f"V_{mi}"], out[f"ret_{mi}"] = U, V, ret
+    np.savez_compressed(os.path.join(HERE, "als_edge_maxit.npz"), source="als_dense_38x45_k5.npz",
+                        meta=json.dumps(_meta(1)), **out)
+    # zero ratings
+    U0, V0 = ref.init_factors(3, 4, 2, 0)
+    U, V, ret = ref.als(np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(0), 2, U0, V0,
+                       max_iteration=7)
+    np.savez_compressed(os.path.join(HERE, "als_edge_zero.npz"), k=2, num_users=3, num_items=4,
+                        U0=U0, V0=V0, U=U, V=V, ret=ret, max_iteration=7,
+                        meta=json.dumps(_meta(1)))
+    # duplicates: a dense 24 x 20 k = 3 fixture with 30 % of the pairs repeated
+    u, i, r, *_ = synth.dense_fixture(24, 20, 3, 0.9, seed=21)
+    rs = np.random.RandomState(21)
+    dup = rs.random_sample(len(u)) < 0.3
+    u2 = np.concatenate([u, u[dup]]).astype(np.int32)
+    i2 = np.concatenate([i, i[dup]]).astype(np.int32)
+    r2 = np.concatenate([r, r[dup] + rs.normal(0, 0.1, dup.sum())])
+    perm = rs.permutation(len(u2))
+    u2, i2, r2 = u2[perm], i2[perm], r2[perm]
+    U0, V0 = ref.init_factors(24, 20, 3, 4)
+    U, V, ret = ref.als(u2, i2, r2, 3, U0, V0)
+    np.savez_compressed(os.path.join(HERE, "als_edge_dups.npz"), user_ids=u2, item_ids=i2,
+                        ratings=r2, k=3, num_users=24, num_items=20, U0=U0, V0=V0, U=U, V=V,
+                        ret=ret, tc_spread=0.0, meta=json.dumps(_meta(1)))
+    # general CG: 40 x 12 sparse, column 5 and rows 3, 17 empty
+    rs = np.random.RandomState(5)
+    A = rs.uniform(-1, 1, (40, 12)) * (rs.random_sample((40, 12)) < 0.4)
+    A[:, 5] = 0
+    A[3, :] = 0
+    A[17, :] = 0
+    b = rs.normal(0, 1, 40)
+    x0 = rs.uniform(-1, 1, 12)
+    rp, ci, v = dense_csr(A)
+    x, it, rr = ref.cg_least_squares(rp, ci, v, 12, b, x0)
+    np.savez_compressed(os.path.join(HERE, "cg_edge_sparse.npz"), row_ptr=rp, col_idx=ci,
+                        vals=v, ncols=12, b=b, x0=x0, x=x, iterations=it, final_rr=rr,
+                        meta=json.dumps(_meta(1)))
+    print("G5 maxit rets", [out[f"ret_{m}"] for m in range(5)], "zero ret", ret, "dups N", len(u2),
+          "cg edge it", it)
+
+
 def g4():
     k = 10
     rs_ = synth.movielens_like("ml-100k", k, seed=synth.DATA_SEED, test_ratio=0.2)
@@ -159,3 +211,4 @@ if __name__ == "__main__":
     g2()
     g3()
     g4()
+    g5()
