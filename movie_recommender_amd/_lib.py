@@ -1,7 +1,8 @@
 """ctypes binding of ``movie_recommender_amd/lib/cpp_ls_lib.so`` (gfx950 HIP).
 
-The shared library exports the reference ABI (``include/cpp_ls_lib.h``) and
-the device-resident engine API (``include/mr_als.h``).  There is no CPU
+The shared library exports the reference ABI (``include/cpp_ls_lib.h``), the
+device-resident engine API (``include/mr_als.h``) and the factor consumers
+(``include/mr_serving.h``).  There is no CPU
 fallback: if the library is missing or cannot load, every entry point raises.
 """
 import ctypes
@@ -111,6 +112,19 @@ SIGNATURES = {
     "mr_als_device_tables": (ctypes.c_int, [VP, ctypes.POINTER(FP), ctypes.POINTER(FP),
                                             ctypes.POINTER(FP), IP]),
     "mr_als_predict": (ctypes.c_int, [VP, ctypes.c_longlong, IP, IP, DP]),
+    # factor consumers (include/mr_serving.h)
+    "mr_rec_create": (VP, [ctypes.c_int, ctypes.c_int, ctypes.c_int, DP, ctypes.c_int, IP, IP,
+                           DP]),
+    "mr_rec_destroy": (None, [VP]),
+    "mr_rec_num_candidates": (ctypes.c_int, [VP]),
+    "mr_rec_fold_in": (ctypes.c_int, [VP, ctypes.c_int, LLP, IP, DP, DP, IP]),
+    "mr_rec_scores": (ctypes.c_int, [VP, ctypes.c_int, DP, DP]),
+    "mr_rec_top_n": (ctypes.c_int, [VP, ctypes.c_int, DP, LLP, IP, ctypes.c_int, IP, DP, IP]),
+    "mr_rec_evaluate": (ctypes.c_int, [VP, ctypes.c_int, DP, ctypes.c_int, IP, LLP, IP, DP, DP,
+                                       LLP, LLP, DP, DP, LLP]),
+    "mr_rank_agreement": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, LLP, DP, DP, DP, LLP,
+                                         LLP]),
+    "mr_rec_last_kernel_ms": (ctypes.c_int, [VP, DP]),
     "mr_last_error": (ctypes.c_char_p, []),
     "mr_device_count": (ctypes.c_int, []),
 }

@@ -7,7 +7,7 @@ import pytest
 
 from conftest import ROOT
 
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("cpp_ls_lib.h", "mr_als.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("cpp_ls_lib.h", "mr_als.h", "mr_serving.h")]
 
 
 def declared_functions():
