@@ -1,0 +1,236 @@
+"""Benchmarks of the factor consumers on MI355X.
+
+    python bench_serving.py [--what topn,eval,foldin] [--reps 3] [--no-cpu]
+
+One JSON line per workload (synthetic data of the ML-full shape, seeded):
+
+* ``topn``   -- recommendation lists per second: for a batch of users, score
+  every movie (the reference's fp64 predict, bit-exact order), drop the
+  user's rated movies, keep the first 400 by (score, movie id)
+  (``recommend.py:86-106``).  50,367 movies x k = 64 (the ML-full training
+  shape of bench.py), 65,536 users, each excluding ~200 rated movies (lognormal list sizes).
+* ``eval``   -- held-out test ratings per second of ``_als_eval``
+  (``worker_process.py:262-306``): prediction + ranking agreement per test
+  user; 103k users, 10 % of the ML-full ratings held out.
+* ``foldin`` -- users per second folded in as ``models.ALS_Model`` does
+  (lstsq on ``[V, 1]`` with the raw ratings), at the app's k = 11
+  (``app_local/als11_*``), 65,536 users with 12-400 ratings.
+
+``value`` is device throughput (sum of the HIP-event kernel times of the
+call, inputs resident in HBM); ``wall_inclusive`` adds the host<->device
+copies of the C-ABI call.  ``roofline`` prices the dominant kernel;
+``cpu_baseline`` times the reference algorithm (``oracle/serving_oracle.py``,
+the reference's own Python control flow with NumPy) on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP64_PEAK_TFS = 78.6     # MI355X FP64 vector peak (FMA = 2 flops)
+HBM_PEAK_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def movie_side(k, n_movies, seed):
+    rs = np.random.RandomState(seed)
+    V = rs.normal(0, 0.35, (n_movies, k))
+    mids = np.sort(rs.choice(np.arange(1, 200_000), n_movies, replace=False))
+    als_ids = {int(m): j for j, m in enumerate(mids)}
+    med = rs.choice(np.arange(1, 11) / 2.0, n_movies)
+    has = rs.random_sample(n_movies) < 0.97
+    medians = {int(m): float(v) for m, v, h in zip(mids, med, has) if h}
+    pop = 1.0 / (1 + rs.permutation(n_movies)) ** 0.9
+    pop /= pop.sum()
+    return V.reshape(-1), als_ids, medians, mids, pop
+
+
+def user_lists(rs, mids, pop, n_users, lo, hi, mean):
+    """Per-user distinct movies, popularity-weighted, lognormal list sizes."""
+    sizes = np.clip(rs.lognormal(np.log(mean), 1.0, n_users).astype(int), lo, hi)
+    draw = (sizes * 1.3).astype(int) + 4
+    cdf = np.cumsum(pop)
+    picks = np.minimum(np.searchsorted(cdf, rs.random_sample(int(draw.sum())) * cdf[-1]),
+                       len(mids) - 1)
+    out, o = [], 0
+    for n, d in zip(sizes, draw):
+        u = np.unique(picks[o:o + d])
+        o += d
+        if len(u) < n:                       # top up with uniform picks
+            extra = rs.choice(len(mids), n * 2, replace=False)
+            u = np.unique(np.concatenate([u, extra]))
+        out.append(mids[rs.permutation(u)[:n]])
+    return out
+
+
+def line(metric, value, unit, cfg, roof, cpu, extra):
+    d = {"metric": metric, "value": value, "unit": unit, "n_gpus": 1,
+         "higher_is_better": True, "dtype": "f64", "data": "synthetic (ML-full shape, seeded)",
+         "config": cfg, "roofline": roof, "cpu_baseline": cpu}
+    d.update(extra)
+    print(json.dumps(d), flush=True)
+
+
+def bench_topn(a):
+    from movie_recommender_amd.serving import MovieTable
+    from oracle import serving_oracle as O
+    k, nm, B, N = 64, 50_367, a.users, 400
+    V, als_ids, medians, mids, pop = movie_side(k, nm, 1)
+    rs = np.random.RandomState(2)
+    X = rs.normal(0, 0.35, (B, k + 1))
+    X[:, k] = rs.normal(0, 0.3, B)
+    rated = user_lists(rs, mids, pop, B, 20, 2000, 120)
+    with MovieTable(k, V, als_ids, medians) as t:
+        nc = t.num_candidates
+        t.top_n_arrays(X[:256], rated[:256], N)                 # warm-up
+        best = None
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            t.top_n_arrays(X, rated, N)
+            wall = time.perf_counter() - t0
+            ms = t.kernel_ms()
+            dev = ms["scores"] + ms["exclude"] + ms["select"]
+            if best is None or dev < best[0]:
+                best = (dev, wall, ms)
+    dev, wall, ms = best
+    flops = B * nc * (2.0 * k + 2)        # k mul + k add + bias + median per score
+    score_tfs = flops / (ms["scores"] * 1e-3) / 1e12
+    sel_bytes = B * nc * 8.0 * 2 + B * nc * 4.0 * 2          # 2 passes over keys + ids
+    roof = {"kernel": "rec_score_kernel", "bound": "fp64-valu", "achieved": round(score_tfs, 2),
+            "peak": FP64_PEAK_TFS, "unit": "TFLOP/s", "frac": round(score_tfs / FP64_PEAK_TFS, 4),
+            "traffic": None,
+            "note": "exact reference order forbids FMA: separate v_mul_f64 + v_add_f64, "
+                    "so 0.5 of the FMA-counted peak is the ceiling",
+            "avg_launch_ms": round(ms["scores"], 3),
+            "select_ms": round(ms["select"], 3),
+            "select_GBps_2pass": round(sel_bytes / (ms["select"] * 1e-3) / 1e9, 1)}
+    cpu = None
+    if not a.no_cpu:
+        ns = 6
+        t0 = time.perf_counter()
+        for u in range(ns):
+            O.recommend(X[u], set(int(m) for m in rated[u]), medians, V, als_ids, N)
+        dt = time.perf_counter() - t0
+        cpu = {"value": ns / dt, "unit": "lists/s", "cores": 1, "kind": "port",
+               "sample": f"{ns} users of the same workload through the reference's "
+                         "get_recommendations loop (oracle/serving_oracle.recommend)"}
+    line("recommendation lists/s (top-400 of 50k movies, k=64, rated movies excluded)",
+         B / (dev * 1e-3), "lists/s",
+         {"workload": "top-N", "users": B, "movies": nc, "k": k, "num_results": N},
+         roof, cpu, {"wall_inclusive": B / wall, "kernel_ms": ms})
+
+
+def bench_eval(a):
+    from movie_recommender_amd.serving import MovieTable
+    from oracle import serving_oracle as O
+    k, nm, nu = 64, 50_367, 102_982
+    V, als_ids, medians, mids, pop = movie_side(k, nm, 3)
+    rs = np.random.RandomState(4)
+    U = rs.normal(0, 0.35, nu * (k + 1))
+    lists = user_lists(rs, mids, pop, nu, 2, 1500, 12)
+    tests = [[(int(m), float(r)) for m, r in zip(l, rs.choice(np.arange(1, 11) / 2.0, len(l)))]
+             for l in lists]
+    rows = np.arange(nu, dtype=np.int32)
+    n_r = sum(len(l) for l in tests)
+    with MovieTable(k, V, als_ids, medians) as t:
+        t.evaluate(U, rows[:100], tests[:100])
+        best = None
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            res = t.evaluate(U, rows, tests)
+            wall = time.perf_counter() - t0
+            ms = t.kernel_ms()["evaluate"]
+            if best is None or ms < best[0]:
+                best = (ms, wall)
+    ms, wall = best
+    pairs = float(sum(len(l) ** 2 for l in tests))
+    byts = n_r * (k * 8.0 + 8 + 4 + 8 + 8)        # gathered movie row + median + id + rating + pred
+    roof = {"kernel": "rec_eval_kernel", "bound": "hbm", "achieved": round(byts / (ms * 1e-3) / 1e9, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+            "pair_comparisons": pairs, "avg_launch_ms": round(ms, 3)}
+    cpu = None
+    if not a.no_cpu:
+        ns = 3000
+        ids = {u: u for u in range(ns)}
+        t0 = time.perf_counter()
+        O.als_eval([(u, tests[u]) for u in range(ns)], medians, U, ids, V, als_ids, k)
+        dt = time.perf_counter() - t0
+        cpu = {"value": sum(len(tests[u]) for u in range(ns)) / dt, "unit": "test ratings/s",
+               "cores": 1, "kind": "port",
+               "sample": f"first {ns} test users through the reference's _als_eval loop "
+                         "(oracle/serving_oracle.als_eval)"}
+    line("held-out test ratings/s evaluated (prediction + ranking agreement, k=64)",
+         n_r / (ms * 1e-3), "test ratings/s",
+         {"workload": "evaluation", "test_users": nu, "test_ratings": n_r, "k": k},
+         roof, cpu, {"wall_inclusive": n_r / wall,
+                     "users_with_agreement": int(np.isfinite(res["agreement"]).sum())})
+
+
+def bench_foldin(a):
+    from movie_recommender_amd.serving import MovieTable
+    from oracle import serving_oracle as O
+    k, nm, B = 11, 22_809, a.users
+    V, als_ids, medians, mids, pop = movie_side(k, nm, 5)
+    rs = np.random.RandomState(6)
+    lists = user_lists(rs, mids, pop, B, k + 1, 400, 60)
+    lists = [[(int(m), float(r)) for m, r in zip(l, rs.choice(np.arange(1, 11) / 2.0, len(l)))]
+             for l in lists]
+    rows = sum(len(l) for l in lists)
+    with MovieTable(k, V, als_ids, medians) as t:
+        t.fold_in(lists[:100])
+        best = None
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            valid, X, method = t.fold_in(lists)
+            wall = time.perf_counter() - t0
+            ms = t.kernel_ms()
+            dev = ms["fold_in"] + ms["fold_in_svd"]
+            if best is None or dev < best[0]:
+                best = (dev, wall, ms, int((method == 2).sum()))
+    dev, wall, ms, n_svd = best
+    K = k + 1
+    flops = rows * 2.0 * (K * (K + 1) / 2 + K) + B * (K ** 3 / 3.0)
+    tfs = flops / (ms["fold_in"] * 1e-3) / 1e12
+    roof = {"kernel": "fold_in_kernel", "bound": "fp64-valu", "achieved": round(tfs, 3),
+            "peak": FP64_PEAK_TFS, "unit": "TFLOP/s", "frac": round(tfs / FP64_PEAK_TFS, 4),
+            "traffic": None, "avg_launch_ms": round(ms["fold_in"], 3), "svd_users": n_svd}
+    cpu = None
+    if not a.no_cpu:
+        ns = 2000
+        t0 = time.perf_counter()
+        for u in range(ns):
+            O.fold_in(k, lists[u], V, als_ids)
+        dt = time.perf_counter() - t0
+        cpu = {"value": ns / dt, "unit": "users/s", "cores": 1, "kind": "port",
+               "sample": f"first {ns} users through models.ALS_Model's fold-in "
+                         "(oracle/serving_oracle.fold_in: numpy.linalg.lstsq)"}
+    line("users folded in per second (ALS_Model lstsq, k=11)", B / (dev * 1e-3), "users/s",
+         {"workload": "fold-in", "users": B, "ratings": rows, "k": k}, roof, cpu,
+         {"wall_inclusive": B / wall})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--what", default="topn,eval,foldin")
+    ap.add_argument("--users", type=int, default=65536)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--no-cpu", action="store_true")
+    a = ap.parse_args()
+    for w in a.what.split(","):
+        t0 = time.time()
+        {"topn": bench_topn, "eval": bench_eval, "foldin": bench_foldin}[w](a)
+        log(f"[bench_serving] {w} done in {time.time() - t0:.1f}s")
+
+
+if __name__ == "__main__":
+    main()

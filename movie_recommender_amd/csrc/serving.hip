@@ -83,7 +83,7 @@ template <bool KEYS>
 __global__ __launch_bounds__(256) void rec_score_kernel(
     int n_users, int n_cand, int k, const double* __restrict__ X,
     const double* __restrict__ Vc, const double* __restrict__ med, void* __restrict__ out,
-    int64_t ld) {
+    int64_t ld, unsigned long long* __restrict__ kmin, unsigned long long* __restrict__ kmax) {
   __shared__ double xs[SC_U][SC_KC];
   __shared__ double vs[SC_C][SC_KC + 1];
   const int tid = threadIdx.x, tx = tid & 63, ty = tid >> 6;
@@ -93,15 +93,23 @@ __global__ __launch_bounds__(256) void rec_score_kernel(
   for (int p = 0; p < 8; ++p)
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[p][q] = 0.0;
+  // staging: thread owns factor column jj = tid & 15 of rows (tid >> 4) + 16 i
+  const int jj = tid & 15, rr = tid >> 4;
   for (int j0 = 0; j0 < k; j0 += SC_KC) {
     const int kc = min(SC_KC, k - j0);
-    for (int e = tid; e < SC_C * SC_KC; e += 256) {
-      const int r = e / SC_KC, j = e % SC_KC, c = c0 + r;
-      vs[r][j] = (c < n_cand && j < kc) ? Vc[(int64_t)c * k + j0 + j] : 0.0;
+    const bool jok = jj < kc;
+    const double* src = Vc + (int64_t)(c0 + rr) * k + j0 + jj;
+#pragma unroll 4
+    for (int i = 0; i < SC_C / 16; ++i) {
+      const bool ok = jok && (c0 + rr + 16 * i) < n_cand;
+      vs[rr + 16 * i][jj] = ok ? src[(int64_t)16 * i * k] : 0.0;
     }
-    for (int e = tid; e < SC_U * SC_KC; e += 256) {
-      const int r = e / SC_KC, j = e % SC_KC, u = u0 + r;
-      xs[r][j] = (u < n_users && j < kc) ? X[(int64_t)u * (k + 1) + j0 + j] : 0.0;
+    if (tid < SC_U * SC_KC / 2) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = rr + 16 * i, u = u0 + r;
+        xs[r][jj] = (jok && u < n_users) ? X[(int64_t)u * (k + 1) + j0 + jj] : 0.0;
+      }
     }
     __syncthreads();
     for (int j = 0; j < kc; ++j) {
@@ -110,28 +118,61 @@ __global__ __launch_bounds__(256) void rec_score_kernel(
       for (int p = 0; p < 8; ++p) xv[p] = xs[ty * 8 + p][j];
 #pragma unroll
       for (int q = 0; q < 4; ++q) vv[q] = vs[tx + 64 * q][j];
+      // products first (16 independent multiplies in flight), then the adds
 #pragma unroll
-      for (int p = 0; p < 8; ++p)
+      for (int h = 0; h < 2; ++h) {
+        double pr[4][4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[p][q] = add_rn(acc[p][q], mul_rn(xv[p], vv[q]));
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) pr[p][q] = mul_rn(xv[4 * h + p], vv[q]);
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[4 * h + p][q] = add_rn(acc[4 * h + p][q], pr[p][q]);
+      }
     }
     __syncthreads();
   }
 #pragma unroll
   for (int p = 0; p < 8; ++p) {
-    const int u = u0 + ty * 8 + p;
+    const int u = u0 + ty * 8 + p;   // wave-uniform
     if (u >= n_users) continue;
     const double bias = X[(int64_t)u * (k + 1) + k];
+    unsigned long long lo = ~0ull, hi = 0ull;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int c = c0 + tx + 64 * q;
       if (c >= n_cand) continue;
       const double s = add_rn(add_rn(acc[p][q], bias), med[c]);
-      if constexpr (KEYS)
-        reinterpret_cast<uint64_t*>(out)[(int64_t)u * ld + c] = score_key(s);
-      else
+      if constexpr (KEYS) {
+        const uint64_t key = score_key(s);
+        reinterpret_cast<uint64_t*>(out)[(int64_t)u * ld + c] = key;
+        lo = min(lo, (unsigned long long)key);
+        hi = max(hi, (unsigned long long)key);
+      } else {
         reinterpret_cast<double*>(out)[(int64_t)u * ld + c] = s;
+      }
     }
+    if constexpr (KEYS) {   // per-user key range: the select skips the common prefix
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, (unsigned long long)__shfl_xor(lo, o, 64));
+        hi = max(hi, (unsigned long long)__shfl_xor(hi, o, 64));
+      }
+      if (tx == 0) {
+        atomicMin(&kmin[u], lo);
+        atomicMax(&kmax[u], hi);
+      }
+    }
+  }
+}
+
+__global__ void rec_range_init_kernel(int n, unsigned long long* kmin, unsigned long long* kmax) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    kmin[i] = ~0ull;
+    kmax[i] = 0ull;
   }
 }
 
@@ -146,79 +187,116 @@ __global__ __launch_bounds__(256) void rec_exclude_kernel(uint64_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------
-// K-S3: exact top-N per user by MSB radix select on the 96-bit composite
+// K-S3: exact top-N per user by MSB radix select on the composite
 // (score key, movie id) -- the order of Python's sort(reverse=True) on
-// (score, movie_id) tuples -- then a bitonic sort of the <= CAP survivors in
-// LDS.  8-bit digits; the select stops at the first level where every
-// element at or above the current bin fits in CAP.
+// (score, movie_id) tuples, held as a 128-bit integer key:mid:0 -- then a
+// bitonic sort of the <= CAP survivors in LDS.  The select starts at the
+// first bit where the user's smallest and largest keys differ (the score
+// kernel records the range), takes 11-bit digits, and stops at the first
+// level where every element at or above the boundary bin fits in CAP; on
+// MovieLens-like scores that is one histogram pass and one collect pass.
 // ---------------------------------------------------------------------------
-constexpr int SEL_NT = 512, SEL_CAP = 2048;
+constexpr int SEL_NT = 512, SEL_CAP = 2048, SEL_D = 11, SEL_BINS = 1 << SEL_D;
+typedef unsigned __int128 u128;
 
-__device__ __forceinline__ uint32_t comp_digit(uint64_t key, uint32_t mid, int d) {
-  return d < 8 ? (uint32_t)(key >> (56 - 8 * d)) & 255u : (mid >> (24 - 8 * (d - 8))) & 255u;
+__device__ __forceinline__ u128 composite(uint64_t key, uint32_t mid) {
+  return ((u128)key << 64) | ((u128)mid << 32);
 }
 
 __global__ __launch_bounds__(SEL_NT) void rec_select_kernel(
     const uint64_t* __restrict__ keys, int64_t ld, int n_cand, const int* __restrict__ mid,
+    const unsigned long long* __restrict__ kmin, const unsigned long long* __restrict__ kmax,
     int N, int* __restrict__ out_mid, double* __restrict__ out_score,
     int* __restrict__ out_count) {
-  __shared__ uint32_t hist[256];
+  __shared__ uint32_t hist[SEL_BINS];
   __shared__ uint64_t ck[SEL_CAP];
   __shared__ uint32_t cm[SEL_CAP];
   __shared__ int s_b, s_stop, s_n;
   __shared__ long long s_gt;
   const int u = blockIdx.x, tid = threadIdx.x;
   const uint64_t* K = keys + (int64_t)u * ld;
-  uint64_t P_hi = 0, M_hi = 0;   // fixed digits so far (value, mask)
-  uint32_t P_lo = 0, M_lo = 0;
-  long long above = 0;           // elements strictly above the prefix range
-  int level = 0;
-  for (; level < 12; ++level) {
-    for (int i = tid; i < 256; i += SEL_NT) hist[i] = 0;
+  // Fast path: SEL_BINS equal-width score bins over the user's [min, max]
+  // (a monotone map, so the boundary bin is exact); one histogram pass, then
+  // collect bins >= boundary if they fit.  Else the radix select below.
+  const double smin = key_score(kmin[u]), smax = key_score(kmax[u]);
+  const double scale = (double)SEL_BINS / (smax - smin);
+  const bool lin = smax > smin && isfinite(scale);
+  auto bin_of = [&](uint64_t key) {
+    return min(SEL_BINS - 1, (int)((key_score(key) - smin) * scale));
+  };
+  int lin_b = -1;
+  if (lin) {
+    for (int i = tid; i < SEL_BINS; i += SEL_NT) hist[i] = 0;
+    __syncthreads();
+    for (int c = tid; c < n_cand; c += SEL_NT) {
+      const uint64_t key = K[c];
+      if (key != 0) atomicAdd(&hist[bin_of(key)], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      long long cum = 0;
+      int b = SEL_BINS - 1;
+      for (; b > 0; --b) {
+        if (cum + hist[b] >= N) break;
+        cum += hist[b];
+      }
+      s_b = (cum + hist[b] <= SEL_CAP) ? b : -1;
+    }
+    __syncthreads();
+    lin_b = s_b;
+    __syncthreads();
+  }
+  // bits above `pos` (counted from the MSB of the 128-bit composite) are
+  // common to every element: the first differing bit of the key range, or the
+  // movie-id part when all keys are equal
+  const uint64_t dk = kmin[u] ^ kmax[u];
+  int pos = dk ? __clzll((long long)dk) : 64;
+  u128 P = composite(kmin[u], 0) & ~(~(u128)0 >> pos);   // common prefix
+  u128 Msk = ~(~(u128)0 >> pos);
+  long long above = 0;   // elements strictly above the prefix range
+  while (lin_b < 0) {
+    const int D = min(SEL_D, 96 - pos);
+    const int sh = 128 - pos - D;
+    for (int i = tid; i < SEL_BINS; i += SEL_NT) hist[i] = 0;
     __syncthreads();
     for (int c = tid; c < n_cand; c += SEL_NT) {
       const uint64_t key = K[c];
       if (key == 0) continue;
-      const uint32_t m = (uint32_t)mid[c];
-      if ((key & M_hi) != P_hi || (m & M_lo) != P_lo) continue;
-      atomicAdd(&hist[comp_digit(key, m, level)], 1u);
+      const u128 x = composite(key, (uint32_t)mid[c]);
+      if ((x & Msk) != P) continue;
+      atomicAdd(&hist[(uint32_t)(x >> sh) & ((1u << D) - 1)], 1u);
     }
     __syncthreads();
     if (tid == 0) {
       long long cum = 0;   // elements in bins above b
-      int b = 255;
+      int b = (1 << D) - 1;
       for (; b > 0; --b) {   // ends at bin 0 when fewer than N remain: take all
         if (above + cum + hist[b] >= N) break;
         cum += hist[b];
       }
-      const long long ge = cum + hist[b];
       s_b = b;
       s_gt = cum;
-      s_stop = (above + ge <= SEL_CAP) ? 1 : 0;
+      s_stop = (above + cum + hist[b] <= SEL_CAP || pos + D >= 96) ? 1 : 0;
     }
     __syncthreads();
     const int b = s_b;
+    P |= (u128)b << sh;   // lower bound of the boundary bin (lower bits zero)
+    Msk |= (((u128)1 << D) - 1) << sh;
+    pos += D;
     const bool stop = s_stop != 0;
-    // extend the prefix with digit b (also for the stop level: lower bound)
-    if (level < 8) {
-      P_hi |= (uint64_t)b << (56 - 8 * level);
-      M_hi |= 255ull << (56 - 8 * level);
-    } else {
-      P_lo |= (uint32_t)b << (24 - 8 * (level - 8));
-      M_lo |= 255u << (24 - 8 * (level - 8));
-    }
-    if (stop) break;
-    above += s_gt;
+    const long long gt = s_gt;
     __syncthreads();
+    if (stop) break;
+    above += gt;
   }
-  // collect every element with composite >= (P_hi, P_lo) (lower bits zero)
+  // collect every element with composite >= P
   if (tid == 0) s_n = 0;
   __syncthreads();
   for (int c = tid; c < n_cand; c += SEL_NT) {
     const uint64_t key = K[c];
     if (key == 0) continue;
     const uint32_t m = (uint32_t)mid[c];
-    if (key > P_hi || (key == P_hi && m >= P_lo)) {
+    if (lin_b >= 0 ? bin_of(key) >= lin_b : composite(key, m) >= P) {
       const int slot = atomicAdd(&s_n, 1);
       if (slot < SEL_CAP) {
         ck[slot] = key;
@@ -710,7 +788,8 @@ static int rec_scores(Rec* r, int n_users, const double* Xh, double* out) {
     const dim3 grid((r->n_cand + SC_C - 1) / SC_C, (nb + SC_U - 1) / SC_U);
     if (timed(r, RT_SCORE, [&]() {
           rec_score_kernel<false><<<grid, 256, 0, r->stream>>>(nb, r->n_cand, r->k, X.p, r->Vc,
-                                                               r->med, S.p, r->n_cand);
+                                                               r->med, S.p, r->n_cand, nullptr,
+                                                               nullptr);
           return 0;
         }))
       return -1;
@@ -736,10 +815,11 @@ static int rec_top_n(Rec* r, int n_users, const double* Xh, const long long* exc
   const int64_t B = std::min<int64_t>(user_chunk(r), n_users);
   DBuf<double> X, osc;
   DBuf<uint64_t> S;
+  DBuf<unsigned long long> kmin, kmax;
   DBuf<int> omid, ocnt, ecand;
   DBuf<int64_t> eoff;
   if (X.alloc(B * K) || S.alloc(B * r->n_cand) || osc.alloc(B * N) || omid.alloc(B * N) ||
-      ocnt.alloc(B) || eoff.alloc(B + 1))
+      ocnt.alloc(B) || eoff.alloc(B + 1) || kmin.alloc(B) || kmax.alloc(B))
     return -1;
   int64_t max_ex = 0;
   if (excl_off) {
@@ -757,8 +837,10 @@ static int rec_top_n(Rec* r, int n_users, const double* Xh, const long long* exc
     MR_HIP(hipMemcpyAsync(X.p, Xh + u0 * K, (size_t)nb * K * 8, hipMemcpyHostToDevice, r->stream));
     const dim3 grid((r->n_cand + SC_C - 1) / SC_C, (nb + SC_U - 1) / SC_U);
     if (timed(r, RT_SCORE, [&]() {
+          rec_range_init_kernel<<<(nb + 255) / 256, 256, 0, r->stream>>>(nb, kmin.p, kmax.p);
           rec_score_kernel<true><<<grid, 256, 0, r->stream>>>(nb, r->n_cand, r->k, X.p, r->Vc,
-                                                              r->med, S.p, r->n_cand);
+                                                              r->med, S.p, r->n_cand, kmin.p,
+                                                              kmax.p);
           return 0;
         }))
       return -1;
@@ -776,8 +858,9 @@ static int rec_top_n(Rec* r, int n_users, const double* Xh, const long long* exc
         return -1;
     }
     if (timed(r, RT_SELECT, [&]() {
-          rec_select_kernel<<<nb, SEL_NT, 0, r->stream>>>(S.p, r->n_cand, r->n_cand, r->mid, N,
-                                                          omid.p, osc.p, ocnt.p);
+          rec_select_kernel<<<nb, SEL_NT, 0, r->stream>>>(S.p, r->n_cand, r->n_cand, r->mid,
+                                                          kmin.p, kmax.p, N, omid.p, osc.p,
+                                                          ocnt.p);
           return 0;
         }))
       return -1;

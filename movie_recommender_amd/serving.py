@@ -149,6 +149,13 @@ class MovieTable:
         ``num_results`` movies by (score, movie id) descending that are not in
         ``rated[u]`` (any container of movie ids).  Returns a list of
         ``[(score, movie_id)]``."""
+        mids, sc, cnt = self.top_n_arrays(X, rated, num_results)
+        return [list(zip(sc[u, :cnt[u]].tolist(), mids[u, :cnt[u]].tolist()))
+                for u in range(len(cnt))]
+
+    def top_n_arrays(self, X, rated=None, num_results=ROTATION_SIZE * 100):
+        """``top_n`` as arrays: movie ids int32[B, n], scores f64[B, n] and
+        the count per user (row u is valid up to count[u])."""
         X = np.ascontiguousarray(np.atleast_2d(X), np.float64)
         B, N = X.shape[0], int(num_results)
         excl_off = excl = None
@@ -165,7 +172,7 @@ class MovieTable:
             self._h, B, _dp(X), _llp(excl_off) if excl_off is not None else None,
             _ip(excl) if excl is not None else None, N, _ip(mids), _dp(sc), _ip(cnt)),
             "mr_rec_top_n")
-        return [[(float(sc[u, i]), int(mids[u, i])) for i in range(cnt[u])] for u in range(B)]
+        return mids, sc, cnt
 
     # -- evaluation -----------------------------------------------------------
     def evaluate(self, U, user_rows, test_lists):

@@ -187,3 +187,20 @@ def test_fold_in_sizes(gpu, k):
         assert ok and valid[u]
         assert rel_err(X[u], x) <= 1e-7, (u, method[u], np.linalg.cond(
             np.c_[V.reshape(-1, k)[[als_ids[m] for m, _ in l]], np.ones(len(l))]))
+
+
+def test_top_n_all_scores_equal(gpu):
+    """Every score identical (zero user, one median): the order is by movie id
+    descending, through the radix-select path (no score range)."""
+    from movie_recommender_amd.serving import MovieTable
+    k = 8
+    V, als_ids, med = synthetic_table(k, 5000, 0, seed=9, ties=0)
+    med = {m: 3.0 for m in med}
+    with MovieTable(k, V, als_ids, med) as t:
+        X = np.zeros((3, k + 1))
+        got = t.top_n(X, [set(), {max(als_ids)}, set(list(als_ids)[:4990])], 400)
+    ids = sorted(als_ids, reverse=True)
+    assert got[0] == [(3.0, m) for m in ids[:400]]
+    assert got[1] == [(3.0, m) for m in ids[1:401]]
+    rest = sorted(set(als_ids) - set(list(als_ids)[:4990]), reverse=True)
+    assert got[2] == [(3.0, m) for m in rest]
