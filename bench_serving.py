@@ -1,4 +1,4 @@
-"""Benchmarks of the factor consumers on MI355X.
+"""Benchmarks of the SURVEY.md 8(f) rows beside the ALS core, on MI355X.
 
     python bench_serving.py [--what topn,eval,foldin] [--reps 3] [--no-cpu]
 
@@ -15,6 +15,10 @@ One JSON line per workload (synthetic data of the ML-full shape, seeded):
 * ``foldin`` -- users per second folded in as ``models.ALS_Model`` does
   (lstsq on ``[V, 1]`` with the raw ratings), at the app's k = 11
   (``app_local/als11_*``), 65,536 users with 12-400 ratings.
+* ``prep``   -- training ratings per second through the ALS data preparation
+  (``movie_lens_data.py:547-680``): medians, the in-place shrink for the
+  reference's factors (3, 5, 7, 9, 11), first-appearance id order and the
+  training arrays, on the ML-full raw shape (27.75 M ratings before shrink).
 
 ``value`` is device throughput (sum of the HIP-event kernel times of the
 call, inputs resident in HBM); ``wall_inclusive`` adds the host<->device
@@ -219,16 +223,85 @@ def bench_foldin(a):
          {"wall_inclusive": B / wall})
 
 
+def bench_prep(a):
+    from movie_recommender_amd import synth
+    from movie_recommender_amd.prep import TrainingSet, _reference_set_order
+    from oracle import prep_oracle as O
+    nu, ni, nd = synth.SHAPES["ml-full"]
+    u, i, r = synth.raw_pairs(nu, ni, nd)
+    order = np.lexsort((np.random.RandomState(1).random_sample(len(u)), u))  # user lists
+    u, i, r = u[order].astype(np.int32), i[order].astype(np.int32), r[order]
+    factors = [3, 5, 7, 9, 11]
+    n = len(r)
+    best = None
+    for _ in range(a.reps):
+        t0 = time.perf_counter()
+        with TrainingSet(u, i, r) as ts:
+            ms = 0.0
+            med = ts.medians()
+            ms += ts.last_ms()
+            for j, k in enumerate(factors):
+                keep, rounds, nk, nus, nms = ts.shrink(k, restart=(j == 0))
+                ms += ts.last_ms()
+                per = ts.first_appearance(np.array([0, n], np.int64))
+                ms += ts.last_ms()
+                mo = _reference_set_order([per[0][1]])
+                uo = _reference_set_order([per[0][0]])
+                umap = np.full(ts.user_bound, -1, np.int32)
+                mmap = np.full(ts.movie_bound, -1, np.int32)
+                umap[uo] = np.arange(len(uo), dtype=np.int32)
+                mmap[mo] = np.arange(len(mo), dtype=np.int32)
+                ts.convert(umap, mmap, np.nan_to_num(med))
+                ms += ts.last_ms()
+                conv_ms = ts.last_ms()
+        wall = time.perf_counter() - t0
+        if best is None or ms < best[0]:
+            best = (ms, wall, nk, nus, nms, conv_ms)
+    ms, wall, nk, nus, nms, conv_ms = best
+    # dominant call: the training-array build (flag -> scan -> scatter); bytes
+    # = alive flag, 8-byte flag and position, ids and rating read per input
+    # rating + 16 B written per kept rating
+    byts = n * (1 + 8 + 8 + 4 + 4 + 8) + nk * 16.0
+    roof = {"kernel": "mr_prep_convert (flag scan + prep_convert_kernel)", "bound": "hbm",
+            "achieved": round(byts / (conv_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(byts / (conv_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "traffic": None, "avg_call_ms": round(conv_ms, 3), "total_device_ms": round(ms, 3)}
+    cpu = None
+    if not a.no_cpu:
+        # the reference's Python loop on a user sample (one process)
+        users = np.unique(u)
+        pick = np.random.RandomState(3).choice(users, len(users) // 50, replace=False)
+        sel = np.isin(u, pick)
+        lists, cur, lst = [], None, None
+        for uu, mm, rr in zip(u[sel].tolist(), i[sel].tolist(), r[sel].tolist()):
+            if uu != cur:
+                cur, lst = uu, []
+                lists.append((uu, lst))
+            lst.append((mm, rr))
+        ns = sum(len(l) for _, l in lists)
+        t0 = time.perf_counter()
+        med_s = O.movie_medians(lists)
+        O.als_data_set_shrink([lists], [None], med_s, factors)
+        dt = time.perf_counter() - t0
+        cpu = {"value": ns / dt, "unit": "ratings/s", "cores": 1, "kind": "port",
+               "sample": f"{len(lists)} users (2 %), {ns} ratings through the reference's "
+                         "preparation loop (oracle/prep_oracle, one process)"}
+    line("training ratings/s prepared (medians + shrink for k=3,5,7,9,11 + id maps + arrays)",
+         n / (ms * 1e-3), "ratings/s",
+         {"workload": "prep", "ratings": n, "factors": factors, "kept_k11": nk,
+          "users_k11": nus, "movies_k11": nms}, roof, cpu, {"wall_inclusive": n / wall})
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--what", default="topn,eval,foldin")
+    ap.add_argument("--what", default="topn,eval,foldin,prep")
     ap.add_argument("--users", type=int, default=65536)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true")
     a = ap.parse_args()
     for w in a.what.split(","):
         t0 = time.time()
-        {"topn": bench_topn, "eval": bench_eval, "foldin": bench_foldin}[w](a)
+        {"topn": bench_topn, "eval": bench_eval, "foldin": bench_foldin, "prep": bench_prep}[w](a)
         log(f"[bench_serving] {w} done in {time.time() - t0:.1f}s")
 
 

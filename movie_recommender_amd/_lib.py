@@ -1,8 +1,9 @@
 """ctypes binding of ``movie_recommender_amd/lib/cpp_ls_lib.so`` (gfx950 HIP).
 
 The shared library exports the reference ABI (``include/cpp_ls_lib.h``), the
-device-resident engine API (``include/mr_als.h``) and the factor consumers
-(``include/mr_serving.h``).  There is no CPU
+device-resident engine API (``include/mr_als.h``), the factor consumers
+(``include/mr_serving.h``) and the training-set preparation
+(``include/mr_prep.h``).  There is no CPU
 fallback: if the library is missing or cannot load, every entry point raises.
 """
 import ctypes
@@ -125,6 +126,16 @@ SIGNATURES = {
     "mr_rank_agreement": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, LLP, DP, DP, DP, LLP,
                                          LLP]),
     "mr_rec_last_kernel_ms": (ctypes.c_int, [VP, DP]),
+    # training-set preparation (include/mr_prep.h)
+    "mr_prep_create": (VP, [ctypes.c_int, ctypes.c_longlong, IP, IP, DP]),
+    "mr_prep_destroy": (None, [VP]),
+    "mr_prep_id_bounds": (ctypes.c_int, [VP, IP, IP]),
+    "mr_prep_medians": (ctypes.c_int, [VP, DP]),
+    "mr_prep_shrink": (ctypes.c_int, [VP, ctypes.c_int, ctypes.c_int,
+                                      ctypes.POINTER(ctypes.c_ubyte), IP, LLP, IP, IP]),
+    "mr_prep_first_appearance": (ctypes.c_int, [VP, ctypes.c_int, LLP, LLP, LLP]),
+    "mr_prep_convert": (ctypes.c_int, [VP, IP, IP, DP, IP, IP, DP]),
+    "mr_prep_last_ms": (ctypes.c_double, [VP]),
     "mr_last_error": (ctypes.c_char_p, []),
     "mr_device_count": (ctypes.c_int, []),
 }

@@ -1,0 +1,89 @@
+"""GPU parity of the ALS training-set preparation (include/mr_prep.h via
+movie_recommender_amd/prep.py) against the reference fixtures and the oracle.
+Everything is exact: integer work, one correctly rounded median and one
+subtraction per rating."""
+import copy
+import os
+import pickle
+
+import numpy as np
+import pytest
+
+from oracle import prep_oracle as O
+from prep_cases import expected_test, fixture
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("p", [1, 3])
+def test_medians_exact(gpu, p):
+    from movie_recommender_amd import prep
+    d = fixture(p)
+    got = prep.movie_medians(d["train"])
+    assert got == d["medians"] and list(got) == list(d["medians"])
+
+
+@pytest.mark.parametrize("p", [1, 3])
+def test_shrink_matches_reference(gpu, p, tmp_path):
+    from movie_recommender_amd import prep
+    d = fixture(p)
+    res = prep.als_data_set_shrink(d["train"], d["test"], d["medians"], d["factors"].tolist(),
+                                   cpu_count=p, out_dir=str(tmp_path))
+    for k in d["factors"].tolist():
+        r = res[k]
+        assert list(r.als_user_ids) == d[f"k{k}_user_keys"].tolist()
+        assert list(r.als_movie_ids) == d[f"k{k}_movie_keys"].tolist()
+        assert np.array_equal(r.user_ids_train, d[f"k{k}_u"])
+        assert np.array_equal(r.movie_ids_train, d[f"k{k}_m"])
+        assert np.array_equal(r.ratings_train, d[f"k{k}_r"])
+        assert r.user_ratings_test == expected_test(d, k)
+        assert r.rounds == int(d[f"k{k}_rounds"])
+        # the files als_train / the evaluation read (our own pickles)
+        with open(os.path.join(tmp_path, f"als{k}_user_ratings_train.bin"), "rb") as f:
+            u, m, rr = pickle.load(f)
+        assert np.array_equal(u, d[f"k{k}_u"]) and np.array_equal(rr, d[f"k{k}_r"])
+        with open(os.path.join(tmp_path, f"als{k}_movie_ids.bin"), "rb") as f:
+            assert list(pickle.load(f)) == d[f"k{k}_movie_keys"].tolist()
+
+
+def test_shrink_larger_synthetic_against_oracle(gpu):
+    """20k users, ~1.2 M ratings, 4 simulated processes, factors 10 then 32."""
+    from movie_recommender_amd import prep
+    rs = np.random.RandomState(8)
+    mids = np.sort(rs.choice(np.arange(1, 250_000), 6000, replace=False))
+    pop = 1.0 / (1 + rs.permutation(6000)) ** 0.9
+    pop /= pop.sum()
+    cdf = np.cumsum(pop)
+    train = []
+    for u in np.sort(rs.choice(np.arange(1, 400_000), 20000, replace=False)):
+        n = int(min(3000, max(1, rs.lognormal(3.5, 1.1))))
+        ms = np.unique(np.minimum(np.searchsorted(cdf, rs.random_sample(n)), 5999))
+        train.append((int(u), [(int(mids[j]), float(x)) for j, x in
+                               zip(rs.permutation(ms), rs.choice(np.arange(1, 11) / 2.0, len(ms)))]))
+    med = O.movie_medians(train)
+    assert prep.movie_medians(train) == med
+    counts = O.split_counts(len(train), 4)
+    exp = O.als_data_set_shrink(O.chunk(copy.deepcopy(train), counts), [None] * 4, med, [10, 32])
+    got = prep.als_data_set_shrink(train, None, med, [10, 32], cpu_count=4)
+    for k, uids, mids_, (u, m, r), _ in exp:
+        g = got[k]
+        assert list(g.als_user_ids) == list(uids) and list(g.als_movie_ids) == list(mids_)
+        assert np.array_equal(g.user_ids_train, u) and np.array_equal(g.movie_ids_train, m)
+        assert np.array_equal(g.ratings_train, r)
+
+
+def test_edge_cases(gpu):
+    from movie_recommender_amd import prep
+    # nothing survives: every user has fewer than k+1 ratings
+    train = [(1, [(10, 4.0), (11, 3.0)]), (2, [(10, 5.0)])]
+    res = prep.als_data_set_shrink(train, None, {10: 4.5, 11: 3.0}, [3])
+    assert res[3].als_user_ids == {} and len(res[3].ratings_train) == 0
+    # an empty user list is dropped in the first round
+    train = [(5, []), (6, [(1, 1.0), (2, 2.0), (3, 3.0)]), (7, [(1, 2.0), (2, 2.0), (3, 5.0)])]
+    res = prep.als_data_set_shrink(train, [(5, []), (6, [(9, 1.0)]), (7, [])],
+                                   prep.movie_medians(train), [1])
+    assert set(res[1].als_user_ids) == {6, 7}
+    assert res[1].user_ratings_test == [(6, [(9, 1.0)]), (7, [])]
+    # medians of even counts are the mean of the two middle ratings
+    assert prep.movie_medians([(1, [(4, 1.0), (5, 2.0)]), (2, [(4, 4.0), (5, 2.5)])]) == \
+        {4: 2.5, 5: 2.25}
