@@ -15,6 +15,9 @@ One JSON line per workload (synthetic data of the ML-full shape, seeded):
 * ``foldin`` -- users per second folded in as ``models.ALS_Model`` does
   (lstsq on ``[V, 1]`` with the raw ratings), at the app's k = 11
   (``app_local/als11_*``), 65,536 users with 12-400 ratings.
+* ``similar`` -- similar-movie lists per second (``build_similar_movies_db``:
+  every movie against every movie through co-rating users, genre gate, top
+  20), all 58k movies of the ML-full raw shape (23.3 M ratings).
 * ``prep``   -- training ratings per second through the ALS data preparation
   (``movie_lens_data.py:547-680``): medians, the in-place shrink for the
   reference's factors (3, 5, 7, 9, 11), first-appearance id order and the
@@ -292,16 +295,80 @@ def bench_prep(a):
           "users_k11": nus, "movies_k11": nms}, roof, cpu, {"wall_inclusive": n / wall})
 
 
+def bench_similar(a):
+    from movie_recommender_amd import synth
+    from movie_recommender_amd.similar import SimilarMovieFinder
+    from oracle import similar_oracle as O
+    nu, ni, nd = synth.SHAPES["ml-full"]
+    u, i, r = synth.raw_pairs(nu, ni, nd)
+    order = np.argsort(i, kind="stable")
+    u, i, r = u[order], i[order], r[order]
+    M = int(i.max()) + 1
+    off = np.zeros(M + 1, np.int64)
+    np.cumsum(np.bincount(i, minlength=M), out=off[1:])
+    rs = np.random.RandomState(7)
+    gm = np.zeros(M, np.uint64)
+    for g in range(3):
+        gm |= (np.uint64(1) << rs.randint(0, 20, M).astype(np.uint64))
+    has = (rs.random_sample(M) < 0.99).astype(np.uint8)
+    r2 = np.round(2 * r).astype(np.uint8)
+    ids = np.arange(1, M + 1, dtype=np.int64)
+    with SimilarMovieFinder.from_arrays(ids, off, u, r2, int(u.max()) + 1, gm, has) as f:
+        f.find_many(np.arange(64), 20)
+        best = None
+        for _ in range(max(1, a.reps - 1)):
+            t0 = time.perf_counter()
+            oj, os_, oc = f.find_many(None, 20)
+            wall = time.perf_counter() - t0
+            ms = f.last_ms()
+            if best is None or ms < best[0]:
+                best = (ms, wall)
+    ms, wall = best
+    # algorithmic work: every (query, co-rated movie) contribution = one
+    # entry of a rater's list = sum over users of deg(u)^2
+    deg = np.bincount(u).astype(np.float64)
+    upd = float((deg ** 2).sum())
+    roof = {"kernel": "sim_find_kernel", "bound": "lds-atomics",
+            "achieved": round(upd / (ms * 1e-3) / 1e9, 2), "peak": None,
+            "unit": "G pair-updates/s", "frac": None, "traffic": None,
+            "pair_updates": upd, "avg_launch_ms": round(ms, 2),
+            "note": "two 64-bit LDS atomics + one 5-byte list read per update"}
+    cpu = None
+    if not a.no_cpu:
+        # the reference's find_similar_movie (oracle) over dicts of a 1/8 user sample
+        keep = u % 8 == 0
+        us, is_, rs_ = u[keep], i[keep], r[keep]
+        mr = [(int(m + 1), {}) for m in range(M)]
+        for uu, mm, x in zip(us.tolist(), is_.tolist(), rs_.tolist()):
+            mr[mm][1][uu] = x
+        genres = {int(m + 1): {int(b) for b in range(20) if (int(gm[m]) >> b) & 1}
+                  for m in range(M) if has[m]}
+        t0 = time.perf_counter()
+        nq = 3
+        for q in range(nq):
+            O.find_similar_movie(genres, mr, q, 0.05, 100, 20)
+        dt = time.perf_counter() - t0
+        cpu = {"value": nq / dt, "unit": "lists/s", "cores": 1, "kind": "port",
+               "sample": f"{nq} query movies through the reference's find_similar_movie "
+                         f"(oracle) on a 1/8 user sample ({int(keep.sum())} ratings)"}
+    line("similar-movie lists/s (all movies of ML-full shape, top 20, genre gate)",
+         M / (ms * 1e-3), "lists/s",
+         {"workload": "similar-movies", "movies": M, "users": int(u.max()) + 1,
+          "ratings": int(len(r)), "num_results": 20}, roof, cpu,
+         {"wall_inclusive": M / wall, "movies_with_results": int((oc > 0).sum())})
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--what", default="topn,eval,foldin,prep")
+    ap.add_argument("--what", default="topn,eval,foldin,prep,similar")
     ap.add_argument("--users", type=int, default=65536)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true")
     a = ap.parse_args()
     for w in a.what.split(","):
         t0 = time.time()
-        {"topn": bench_topn, "eval": bench_eval, "foldin": bench_foldin, "prep": bench_prep}[w](a)
+        {"topn": bench_topn, "eval": bench_eval, "foldin": bench_foldin, "prep": bench_prep,
+         "similar": bench_similar}[w](a)
         log(f"[bench_serving] {w} done in {time.time() - t0:.1f}s")
 
 

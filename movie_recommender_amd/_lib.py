@@ -2,8 +2,9 @@
 
 The shared library exports the reference ABI (``include/cpp_ls_lib.h``), the
 device-resident engine API (``include/mr_als.h``), the factor consumers
-(``include/mr_serving.h``) and the training-set preparation
-(``include/mr_prep.h``).  There is no CPU
+(``include/mr_serving.h``), the training-set preparation
+(``include/mr_prep.h``) and the similar-movies database
+(``include/mr_similar.h``).  There is no CPU
 fallback: if the library is missing or cannot load, every entry point raises.
 """
 import ctypes
@@ -136,6 +137,14 @@ SIGNATURES = {
     "mr_prep_first_appearance": (ctypes.c_int, [VP, ctypes.c_int, LLP, LLP, LLP]),
     "mr_prep_convert": (ctypes.c_int, [VP, IP, IP, DP, IP, IP, DP]),
     "mr_prep_last_ms": (ctypes.c_double, [VP]),
+    # similar movies (include/mr_similar.h)
+    "mr_similar_create": (VP, [ctypes.c_int, ctypes.c_int, ctypes.c_int, LLP, IP,
+                               ctypes.POINTER(ctypes.c_ubyte), ctypes.POINTER(ctypes.c_ulonglong),
+                               ctypes.POINTER(ctypes.c_ubyte)]),
+    "mr_similar_destroy": (None, [VP]),
+    "mr_similar_find": (ctypes.c_int, [VP, ctypes.c_int, IP, DP, ctypes.c_int, ctypes.c_int, IP,
+                                       DP, IP]),
+    "mr_similar_last_ms": (ctypes.c_double, [VP]),
     "mr_last_error": (ctypes.c_char_p, []),
     "mr_device_count": (ctypes.c_int, []),
 }

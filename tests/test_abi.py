@@ -7,7 +7,7 @@ import pytest
 
 from conftest import ROOT
 
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("cpp_ls_lib.h", "mr_als.h", "mr_serving.h", "mr_prep.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("cpp_ls_lib.h", "mr_als.h", "mr_serving.h", "mr_prep.h", "mr_similar.h")]
 
 
 def declared_functions():
