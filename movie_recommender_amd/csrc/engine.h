@@ -42,6 +42,8 @@ struct Engine {
   int k = 0, ldk = 0;
   int64_t U = 0, I = 0, N = 0;
   float *Ufac = nullptr, *Ubias = nullptr, *Vfac = nullptr;
+  uint16_t* Fsplit = nullptr;   // bf16x3 copy of the gathered table (gram3)
+  bool use_gram3 = false;
   Side su, si;
   CgState* d_state = nullptr;
   CgState* h_state = nullptr;

@@ -58,7 +58,7 @@ Engine::~Engine() {
     (void)hipStreamSynchronize(stream);
     free_side(su, stream);
     free_side(si, stream);
-    dfree(Ufac, stream); dfree(Ubias, stream); dfree(Vfac, stream);
+    dfree(Ufac, stream); dfree(Ubias, stream); dfree(Vfac, stream); dfree(Fsplit, stream);
     dfree(d_state, stream); dfree(partials, stream); dfree(d_flag, stream);
     (void)hipStreamSynchronize(stream);
     if (h_state) (void)hipHostFree(h_state);
@@ -232,6 +232,15 @@ int Engine::init(int dev, int k_, int64_t U_, int64_t I_, int64_t n_u,
   MR_HIP(hipMemsetAsync(Ufac, 0, (U + 1) * ldk * 4, stream));
   MR_HIP(hipMemsetAsync(Ubias, 0, (U + 1) * 4, stream));
   MR_HIP(hipMemsetAsync(Vfac, 0, (I + 1) * ldk * 4, stream));
+  // bf16x3 matrix-core normal equations (gram3.hip) on request (MR_GRAM3=1):
+  // parity-green, but at k = 64 it measures level with the f32 MFMA kernel
+  // (0.96 / 0.89-1.17 ms vs 0.92-1.0 ms per side), so the f32 kernel stays the
+  // default (DESIGN.md "Gram kernel variants")
+  {
+    const char* e = getenv("MR_GRAM3");
+    use_gram3 = gram3_supported(k) && e && atoi(e) == 1;
+  }
+  if (use_gram3 && dalloc(&Fsplit, (std::max(U, I) + 1) * 3 * ldk, stream)) return -1;
   // upload + build both views
   const bool same = (uv_uid == iv_uid && uv_iid == iv_iid && uv_r == iv_r && n_u == n_i);
   for (int view = 0; view < (same ? 1 : 2); ++view) {
@@ -482,9 +491,16 @@ int Engine::gram(Side& S) {
   hipEvent_t a = nullptr;
   const int cls = user ? MR_K_GRAM_USERS : MR_K_GRAM_ITEMS;
   if (tic(cls, -1, &a)) return -1;
-  if (launch_gram(stream, user, k, S.work, S.n_work, S.idx, S.val, F, bias,
-                  (int)(user ? I : U), direct_dst(S), slab_dst(S)))
+  const int zrow = (int)(user ? I : U);
+  if (use_gram3) {
+    if (launch_split_table(stream, zrow + 1, k, F, Fsplit) ||
+        launch_gram3(stream, user, k, S.work, S.n_work, S.idx, S.val, Fsplit, bias, zrow,
+                     direct_dst(S), slab_dst(S)))
+      return -1;
+  } else if (launch_gram(stream, user, k, S.work, S.n_work, S.idx, S.val, F, bias, zrow,
+                         direct_dst(S), slab_dst(S))) {
     return -1;
+  }
   if (toc(cls, -1, a)) return -1;
   if (S.n_split) {
     if (tic(MR_K_SLAB_REDUCE, -1, &a)) return -1;

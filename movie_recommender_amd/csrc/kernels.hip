@@ -128,7 +128,11 @@ __device__ __forceinline__ void gather_group(float (&a)[G][NB], float (&ww)[G], 
 #pragma unroll
   for (int u = 0; u < G; ++u) {
     const int src = 4 * (step0_in_chunk + u) + q;
+#if defined(MR_GRAM_PROBE) && MR_GRAM_PROBE == 1
+    const int ri = __shfl(cr.idx, src, 64) & 1023;   // probe: cache-resident rows
+#else
     const int ri = __shfl(cr.idx, src, 64);
+#endif
     ww[u] = __shfl(cr.w, src, 64);
     const char* p = Fc + (uint64_t)(uint32_t)ri * row_bytes;
     if constexpr (NB % 4 == 0) {
@@ -167,7 +171,11 @@ __device__ __forceinline__ void mfma_group(floatx4 (&acc)[NB * (NB + 1) / 2],
       for (int bi = 0; bi < NB; ++bi)
 #pragma unroll
         for (int bj = bi; bj < NB; ++bj) {
+#if defined(MR_GRAM_PROBE) && MR_GRAM_PROBE == 2
+          acc[t][0] += a[u][bi] * a[u][bj];   // probe: no MFMA
+#else
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][bi], a[u][bj], acc[t], 0, 0, 0);
+#endif
           ++t;
         }
     }

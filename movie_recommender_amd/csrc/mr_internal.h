@@ -149,6 +149,13 @@ int launch_gram(hipStream_t s, bool user_side, int k, const WorkItem* work,
                 int64_t n_work, const int32_t* idx, const float* val,
                 const float* F, const float* bias, int zrow, GramDst direct,
                 GramDst slab);
+// bf16x3 normal equations (gram3.hip): Fs = launch_split_table(F) once per
+// half-step, rows x 3 parts x ldk bf16 in virtual column order.
+bool gram3_supported(int k);
+int launch_split_table(hipStream_t s, int64_t rows, int k, const float* F, uint16_t* Fs);
+int launch_gram3(hipStream_t s, bool user_side, int k, const WorkItem* work, int64_t n_work,
+                 const int32_t* idx, const float* val, const uint16_t* Fs, const float* bias,
+                 int zrow, GramDst direct, GramDst slab);
 int launch_slab_reduce(hipStream_t s, bool user_side, int k,
                        const SplitItem* split, int64_t n_split,
                        const float* slab, int64_t rec, GramDst direct);

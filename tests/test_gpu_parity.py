@@ -128,10 +128,13 @@ def test_engine_matches_abi_and_is_deterministic(gpu):
     assert np.array_equal(U2, U3) and np.array_equal(V2, V3)   # bitwise reproducible
 
 
-@pytest.mark.parametrize("k", [3, 10, 16, 32, 33, 64, 65, 96, 128])
-def test_gram_kernel_vs_numpy(gpu, k):
+@pytest.mark.parametrize("k,gram3", [(3, 0), (10, 0), (16, 0), (32, 0), (33, 0), (64, 0),
+                                     (65, 0), (96, 0), (128, 0), (20, 1), (32, 1), (64, 1)])
+def test_gram_kernel_vs_numpy(gpu, k, gram3, monkeypatch):
     """Normal equations of both sides against fp64 NumPy, including heavy
-    entities split across waves (chunk 64 forces slabs) and empty entities."""
+    entities split across waves (chunk 64 forces slabs) and empty entities;
+    gram3 = 1 runs the bf16x3 matrix-core kernel (MR_GRAM3=1)."""
+    monkeypatch.setenv("MR_GRAM3", str(gram3))
     from movie_recommender_amd.engine import AlsContext
     from oracle import als_oracle as O
     rng = np.random.default_rng(k)
