@@ -539,6 +539,12 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr) {
   h_init->min_dec = min_dec;
   h_init->max_it = max_it;
   MR_HIP(hipMemcpyAsync(d_state, h_init, sizeof(CgState), hipMemcpyHostToDevice, stream));
+  // Single-GPU runs fold the control steps into the last block of the matvec
+  // (alpha) and of the update (INIT / BETA rules + publish): two kernels per
+  // iteration instead of four.  Sharded runs keep the control kernels, whose
+  // reduce and finalize halves bracket the RCCL all-reduce.
+  const bool fused = !sharded();
+  CgState* fst = fused ? d_state : nullptr;
   // r0 = G x - c ; p0 = -r0 ; rr  (matrix.cpp:464-485)
   hipEvent_t a = nullptr;
   if (tic(mv_cls, -1, &a)) return -1;
@@ -546,33 +552,33 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr) {
                        S.r, S.rb, S.q, S.qb, partials, S.n_part_mv))
     return -1;
   if (toc(mv_cls, -1, a)) return -1;
+  const int seq_init = ++mirror_seq;
   if (tic(MR_K_CG_UPDATE, -1, &a)) return -1;
   if (launch_cg_update(stream, d_state, UPD_INIT, n, nb, xf, S.r, S.p, S.q, S.C, xb,
-                       S.rb, S.pb, S.qb, S.Cb, partials, kUpdParts))
+                       S.rb, S.pb, S.qb, S.Cb, partials, kUpdParts, fst, d_mirror, seq_init))
     return -1;
   if (toc(MR_K_CG_UPDATE, -1, a)) return -1;
   cur_parts = kUpdParts;
-  const int seq_init = ++mirror_seq;
-  if (control(CG_INIT, seq_init)) return -1;
+  if (!fused && control(CG_INIT, seq_init)) return -1;
 
   std::vector<int> seq_of;   // publish seq of iteration t's BETA step
   auto launch_iter = [&](int t) -> int {
     hipEvent_t ev = nullptr;
     if (tic(mv_cls, t, &ev)) return -1;
     if (launch_cg_matvec(stream, user, d_state, t > 0, S.E, k, S.G, S.Gs, S.Gn, S.p, S.pb,
-                         S.r, S.rb, S.q, S.qb, partials, S.n_part_mv))
+                         S.r, S.rb, S.q, S.qb, partials, S.n_part_mv, fst, CG_ALPHA))
       return -1;
     if (toc(mv_cls, t, ev)) return -1;
     cur_parts = S.n_part_mv;
-    if (control(CG_ALPHA, 0)) return -1;
+    if (!fused && control(CG_ALPHA, 0)) return -1;
+    seq_of.push_back(++mirror_seq);
     if (tic(MR_K_CG_UPDATE, t, &ev)) return -1;
     if (launch_cg_update(stream, d_state, UPD_STEP, n, nb, xf, S.r, S.p, S.q, S.C, xb, S.rb,
-                         S.pb, S.qb, S.Cb, partials, kUpdParts))
+                         S.pb, S.qb, S.Cb, partials, kUpdParts, fst, d_mirror, seq_of.back()))
       return -1;
     if (toc(MR_K_CG_UPDATE, t, ev)) return -1;
     cur_parts = kUpdParts;
-    seq_of.push_back(++mirror_seq);
-    return control(CG_BETA, seq_of.back());
+    return fused ? 0 : control(CG_BETA, seq_of.back());
   };
 
   // Iteration 0 cannot stop by stagnation (fails starts at 0) and iteration 1

@@ -455,6 +455,86 @@ int launch_slab_reduce(hipStream_t s, bool user_side, int k,
 // product T^T v_bi into y_bj; the 4-lane row partials and 16-lane column
 // partials are combined once per entity through LDS in a fixed order.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ void publish(const CgState* st, CgMirror* m, int seq) {
+  if (!m) return;
+  m->done = st->done;
+  m->fails = st->fails;
+  m->it = st->it;
+  m->ret = st->ret;
+  m->n_matvec = st->n_matvec;
+  m->rr = st->rr;
+  m->final_rr = st->final_rr;
+  __threadfence_system();
+  __hip_atomic_store(&m->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// INIT / ALPHA / BETA rules on the reduced sum s (one thread).
+__device__ void cg_finalize(CgState* st, int phase, double s, CgMirror* mirror, int seq) {
+  if (phase == CG_INIT) {
+    st->rr = s;
+    st->final_rr = s;
+    st->it = 0;
+    st->fails = 0;
+    st->done = 0;
+    st->ret = 0;
+    if (st->max_it <= 0 || s < 1e-6) st->done = 1;
+    publish(st, mirror, seq);
+  } else if (phase == CG_ALPHA) {
+    st->alpha = st->rr / s;
+    st->n_matvec += 1;
+  } else {
+    const double rr2 = s;
+    st->final_rr = rr2;
+    const double beta = rr2 / st->rr;
+    st->beta = beta;
+    if (beta > 1.0 - st->min_dec) st->fails += 1;
+    else st->fails = 0;
+    if (st->fails >= 2) {
+      st->done = 1;
+      st->ret = st->it;
+    } else {
+      st->rr = rr2;
+      st->it += 1;
+      if (st->it >= st->max_it || rr2 < 1e-6) {
+        st->done = 1;
+        st->ret = st->it;
+      }
+    }
+    publish(st, mirror, seq);
+  }
+}
+
+// Fused control: every block stores its partial sum write-through (sc1) and
+// drains it, then one lane adds to an agent-scope counter; the block whose add
+// returns gridDim.x-1 reduces all partials (sc1 loads, index order -- the
+// control kernel's order, so results are identical) and applies the rules.
+// No L2 writeback fence: __threadfence() here (buffer_wbl2 per block) cost
+// ~90 us per matvec launch.
+__device__ __forceinline__ void store_partial(double* partials, double tot) {
+  if (threadIdx.x == 0)
+    __hip_atomic_store(&partials[blockIdx.x], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ void last_block_finalize(CgState* st, int phase, double* partials, CgMirror* mirror,
+                                    int seq, double* sh) {
+  __shared__ int s_last;
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_last = __hip_atomic_fetch_add(&st->arrive, 1u, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x)
+    acc += __hip_atomic_load(&partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const double tot = block_sum_f64<256>(acc, sh);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(&st->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    cg_finalize(st, phase, tot, mirror, seq);
+  }
+}
+
 constexpr int MV_WAVES = 4;
 
 template <int NB, bool USER, bool NT>
@@ -463,7 +543,8 @@ __global__ __launch_bounds__(256) void cg_matvec_kernel(
     const float* __restrict__ G, const float* __restrict__ Gs,
     const float* __restrict__ Gn, float* __restrict__ v, float* __restrict__ vb,
     const float* __restrict__ r, const float* __restrict__ rb,
-    float* __restrict__ y, float* __restrict__ yb, double* __restrict__ partials) {
+    float* __restrict__ y, float* __restrict__ yb, double* __restrict__ partials,
+    CgState* fst, int phase) {
   if (st->done) return;
   constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2, NTILE = NO + NF + (NB & 1);
   constexpr int64_t GS = (int64_t)NTILE * 256 + NF * 16;   // == gsize_of(k)
@@ -634,7 +715,9 @@ __global__ __launch_bounds__(256) void cg_matvec_kernel(
     __builtin_amdgcn_wave_barrier();
   }
   const double tot = block_sum_f64<256>(lane == 0 ? dsum : 0.0, sh);
-  if (threadIdx.x == 0) partials[blockIdx.x] = tot;
+  if (fst) store_partial(partials, tot);
+  else if (threadIdx.x == 0) partials[blockIdx.x] = tot;
+  if (fst && phase == CG_ALPHA) last_block_finalize(fst, CG_ALPHA, partials, nullptr, 0, sh);
 }
 
 // G streams once per CG iteration and exceeds the Infinity Cache at scale,
@@ -655,11 +738,11 @@ static int launch_matvec_nb(hipStream_t s, bool user_side, const CgState* st, in
                             int64_t E, int k, const float* G, const float* Gs,
                             const float* Gn, float* v, float* vb, const float* r,
                             const float* rb, float* y, float* yb, double* partials,
-                            int n_part) {
+                            int n_part, CgState* fst, int phase) {
   const bool nt = matvec_nt();
 #define MR_MV_LAUNCH(U, N)                                                          \
   cg_matvec_kernel<NB, U, N><<<dim3(n_part), dim3(256), 0, s>>>(                    \
-      st, update_p, E, k, ldk_of(k), G, Gs, Gn, v, vb, r, rb, y, yb, partials)
+      st, update_p, E, k, ldk_of(k), G, Gs, Gn, v, vb, r, rb, y, yb, partials, fst, phase)
   if (user_side) {
     if (nt) MR_MV_LAUNCH(true, true); else MR_MV_LAUNCH(true, false);
   } else {
@@ -674,12 +757,12 @@ int launch_cg_matvec(hipStream_t s, bool user_side, const CgState* st,
                      int update_p, int64_t E, int k, const float* G,
                      const float* Gs, const float* Gn, float* v, float* vb,
                      const float* r, const float* rb, float* y, float* yb,
-                     double* partials, int n_part) {
+                     double* partials, int n_part, CgState* fst, int phase) {
   if (n_part <= 0) return 0;
 #define MR_MV_CASE(NB)                                                               \
   case NB:                                                                           \
     return launch_matvec_nb<NB>(s, user_side, st, update_p, E, k, G, Gs, Gn, v, vb, r, \
-                                rb, y, yb, partials, n_part);
+                                rb, y, yb, partials, n_part, fst, phase);
   switch (nb16_of(k)) {
     MR_MV_CASE(1) MR_MV_CASE(2) MR_MV_CASE(3) MR_MV_CASE(4)
     MR_MV_CASE(5) MR_MV_CASE(6) MR_MV_CASE(7) MR_MV_CASE(8)
@@ -698,7 +781,7 @@ __global__ __launch_bounds__(256) void cg_update_kernel(
     const float* __restrict__ q, const float* __restrict__ c,
     float* __restrict__ xb, float* __restrict__ rb, float* __restrict__ pb,
     const float* __restrict__ qb, const float* __restrict__ cb,
-    double* __restrict__ partials) {
+    double* __restrict__ partials, CgState* fst, CgMirror* mirror, int seq) {
   if (st->done) return;
   __shared__ double sh[4];
   const float alpha = (float)st->alpha;
@@ -747,16 +830,19 @@ __global__ __launch_bounds__(256) void cg_update_kernel(
     }
   }
   const double tot = block_sum_f64<256>(acc, sh);
-  if (threadIdx.x == 0) partials[blockIdx.x] = tot;
+  if (fst) store_partial(partials, tot);
+  else if (threadIdx.x == 0) partials[blockIdx.x] = tot;
+  if (fst)
+    last_block_finalize(fst, mode == UPD_INIT ? CG_INIT : CG_BETA, partials, mirror, seq, sh);
 }
 
 int launch_cg_update(hipStream_t s, const CgState* st, int mode, int64_t n,
                      int64_t nb, float* x, float* r, float* p, const float* q,
                      const float* c, float* xb, float* rb, float* pb,
                      const float* qb, const float* cb, double* partials,
-                     int n_part) {
+                     int n_part, CgState* fst, CgMirror* mirror, int seq) {
   cg_update_kernel<<<dim3(n_part), dim3(256), 0, s>>>(
-      st, mode, n / 4, nb, x, r, p, q, c, xb, rb, pb, qb, cb, partials);
+      st, mode, n / 4, nb, x, r, p, q, c, xb, rb, pb, qb, cb, partials, fst, mirror, seq);
   MR_HIP(hipGetLastError());
   return 0;
 }
@@ -771,18 +857,6 @@ int launch_cg_update(hipStream_t s, const CgState* st, int mode, int64_t n,
 // ctl: CTL_REDUCE sums the local partials into st->comm[0] (sharded runs
 // all-reduce that slot next); CTL_FINALIZE applies the rules from comm[0].
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void publish(const CgState* st, CgMirror* m, int seq) {
-  if (!m) return;
-  m->done = st->done;
-  m->fails = st->fails;
-  m->it = st->it;
-  m->ret = st->ret;
-  m->n_matvec = st->n_matvec;
-  m->rr = st->rr;
-  m->final_rr = st->final_rr;
-  __threadfence_system();
-  __hip_atomic_store(&m->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 
 __global__ __launch_bounds__(256) void cg_control_kernel(
     CgState* __restrict__ st, int phase, int ctl,
@@ -796,39 +870,7 @@ __global__ __launch_bounds__(256) void cg_control_kernel(
     if (threadIdx.x == 0) st->comm[0] = tot;
   }
   if (threadIdx.x != 0 || !(ctl & CTL_FINALIZE)) return;
-  const double s = st->comm[0];
-  if (phase == CG_INIT) {
-    st->rr = s;
-    st->final_rr = s;
-    st->it = 0;
-    st->fails = 0;
-    st->done = 0;
-    st->ret = 0;
-    if (st->max_it <= 0 || s < 1e-6) st->done = 1;
-    publish(st, mirror, seq);
-  } else if (phase == CG_ALPHA) {
-    st->alpha = st->rr / s;
-    st->n_matvec += 1;
-  } else {
-    const double rr2 = s;
-    st->final_rr = rr2;
-    const double beta = rr2 / st->rr;
-    st->beta = beta;
-    if (beta > 1.0 - st->min_dec) st->fails += 1;
-    else st->fails = 0;
-    if (st->fails >= 2) {
-      st->done = 1;
-      st->ret = st->it;
-    } else {
-      st->rr = rr2;
-      st->it += 1;
-      if (st->it >= st->max_it || rr2 < 1e-6) {
-        st->done = 1;
-        st->ret = st->it;
-      }
-    }
-    publish(st, mirror, seq);
-  }
+  cg_finalize(st, phase, st->comm[0], mirror, seq);
 }
 
 int launch_cg_control(hipStream_t s, CgState* st, int phase, int ctl,

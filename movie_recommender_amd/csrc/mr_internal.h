@@ -123,6 +123,8 @@ struct CgState {
   int32_t ret;      // iteration count returned by cg_least_squares
   int32_t max_it;
   int32_t n_matvec; // matvec launches that did work (for kernel timing)
+  uint32_t arrive;  // blocks finished (fused control: the last one finalizes)
+  uint32_t pad;
 };
 
 // Host-visible copy of the CG state, written by cg_control into pinned,
@@ -159,16 +161,21 @@ int launch_gram3(hipStream_t s, bool user_side, int k, const WorkItem* work, int
 int launch_slab_reduce(hipStream_t s, bool user_side, int k,
                        const SplitItem* split, int64_t n_split,
                        const float* slab, int64_t rec, GramDst direct);
+// Fused control (single-GPU runs): fst != nullptr makes the last block of
+// the matvec compute alpha (phase CG_ALPHA) and the last block of the update
+// apply the INIT / BETA rules and publish to `mirror` -- no control kernels.
 int launch_cg_matvec(hipStream_t s, bool user_side, const CgState* st,
                      int update_p, int64_t E, int k, const float* G,
                      const float* Gs, const float* Gn, float* v, float* vb,
                      const float* r, const float* rb, float* y, float* yb,
-                     double* partials, int n_part);
+                     double* partials, int n_part, CgState* fst = nullptr,
+                     int phase = CG_INIT);
 int launch_cg_update(hipStream_t s, const CgState* st, int mode, int64_t n,
                      int64_t nb, float* x, float* r, float* p, const float* q,
                      const float* c, float* xb, float* rb, float* pb,
                      const float* qb, const float* cb, double* partials,
-                     int n_part);
+                     int n_part, CgState* fst = nullptr, CgMirror* mirror = nullptr,
+                     int seq = 0);
 int launch_cg_control(hipStream_t s, CgState* st, int phase, int ctl,
                       const double* partials, int n_part, CgMirror* mirror = nullptr,
                       int seq = 0);
