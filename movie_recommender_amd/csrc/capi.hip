@@ -251,7 +251,7 @@ int mr_als_build_normal_equations(mr_als* ctx, int side) {
   return guarded([&]() -> int {
     MR_HIP(hipSetDevice(ctx->eng.device));
     if (ctx->eng.gram(side == MR_SIDE_USERS ? ctx->eng.su : ctx->eng.si)) return -1;
-    if (ctx->eng.resolve_timing(1 << 30)) return -1;
+    if (ctx->eng.resolve_timing()) return -1;
     MR_HIP(hipStreamSynchronize(ctx->eng.stream));
     return 0;
   });
@@ -267,14 +267,20 @@ int mr_als_get_normal_equations(mr_als* ctx, int side, int n, const int* entitie
 
 int mr_als_get_stats(mr_als* ctx, mr_stats* out) {
   MR_CHECK(ctx && out, "null argument");
-  *out = ctx->eng.stats;
-  return 0;
+  return guarded([&]() {
+    if (ctx->eng.resolve_timing()) return -1;
+    *out = ctx->eng.stats;
+    return 0;
+  });
 }
 
 int mr_als_reset_stats(mr_als* ctx) {
   MR_CHECK(ctx, "null context");
-  ctx->eng.stats = mr_stats{};
-  return 0;
+  return guarded([&]() {
+    if (ctx->eng.resolve_timing()) return -1;   // drop launches timed before the reset
+    ctx->eng.stats = mr_stats{};
+    return 0;
+  });
 }
 
 int mr_als_sync(mr_als* ctx) {

@@ -34,6 +34,15 @@ struct Side {
 struct Pending {
   int cls, tag;
   hipEvent_t a, b;
+  int n_real;   // CG launches with tag >= n_real ran after the solve ended
+};
+
+// One timed phase (Gram or solve of a half-step): pending entries
+// [first, last) plus, in sharded runs, a marker after the RCCL exchange.
+struct PhaseSpan {
+  int phase;
+  size_t first, last;
+  hipEvent_t end;
 };
 
 struct Engine {
@@ -61,6 +70,7 @@ struct Engine {
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
   std::vector<Pending> pending;
+  std::vector<PhaseSpan> spans;
   mr_stats stats{};
   // sharded runs: native RCCL communicator (ncclComm_t) or host callbacks
   void* rccl = nullptr;
@@ -101,7 +111,7 @@ struct Engine {
   int ev_get(hipEvent_t* e);
   int tic(int cls, int tag, hipEvent_t* a);
   int toc(int cls, int tag, hipEvent_t a);
-  int resolve_timing(int n_real);
+  int resolve_timing();
 };
 
 int cg_ls_f64(int device, int rows, int cols, const int* rp, const int* ci,

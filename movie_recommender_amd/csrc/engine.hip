@@ -67,6 +67,7 @@ Engine::~Engine() {
     if (h_mirror) (void)hipHostFree(h_mirror);
     for (auto& e : ev_pool) (void)hipEventDestroy(e);
     for (auto& p : pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
+    for (auto& sp : spans) if (sp.end) (void)hipEventDestroy(sp.end);
     if (rccl) (void)ncclCommDestroy((ncclComm_t)rccl);
     (void)hipStreamDestroy(stream);
   }
@@ -85,40 +86,62 @@ int Engine::ev_get(hipEvent_t* e) {
   return 0;
 }
 
+// Timed launchers: tic hands a (start, stop) event pair to the launch-timing
+// slot (mr_internal.h), which the launcher's kernels record from their own
+// dispatch packets; toc files the pair for resolve_timing.
+thread_local LaunchTiming t_launch;
+
 int Engine::tic(int cls, int tag, hipEvent_t* a) {
-  if (!timing) return 0;
-  if (ev_get(a)) return -1;
-  MR_HIP(hipEventRecord(*a, stream));
   (void)cls; (void)tag;
+  if (!timing) return 0;
+  hipEvent_t b;
+  if (ev_get(a) || ev_get(&b)) return -1;
+  t_launch.start = *a;
+  t_launch.stop = b;
   return 0;
 }
 
 int Engine::toc(int cls, int tag, hipEvent_t a) {
   if (!timing) return 0;
-  hipEvent_t b;
-  if (ev_get(&b)) return -1;
-  MR_HIP(hipEventRecord(b, stream));
-  pending.push_back({cls, tag, a, b});
+  if (t_launch.start) {  // the launcher had nothing to launch: empty interval
+    MR_HIP(hipEventRecord(a, stream));
+    MR_HIP(hipEventRecord(t_launch.stop, stream));
+  }
+  pending.push_back({cls, tag, a, t_launch.stop, 1 << 30});
+  t_launch = LaunchTiming{};
   return 0;
 }
 
-// Attribute pending kernel times.  Launches tagged with a CG iteration index
-// >= n_real ran after the solve had finished (early-exit no-ops) and are not
-// counted as kernel launches.
-int Engine::resolve_timing(int n_real) {
-  if (pending.empty()) return 0;
+// Attribute pending kernel and phase times (one stream sync; called when the
+// stats are read, not per half-step, so timing does not stall the stream).
+// Launches tagged with a CG iteration index >= their solve's n_real ran after
+// the solve had finished (early-exit no-ops) and are not counted.
+int Engine::resolve_timing() {
+  if (pending.empty() && spans.empty()) return 0;
   MR_HIP(hipStreamSynchronize(stream));
   for (auto& p : pending) {
-    if (p.tag < 0 || p.tag < n_real) {
+    if (p.tag < 0 || p.tag < p.n_real) {
       float ms = 0.f;
       MR_HIP(hipEventElapsedTime(&ms, p.a, p.b));
       stats.kernel_ms[p.cls] += ms;
       stats.kernel_launches[p.cls] += 1;
     }
+  }
+  for (auto& sp : spans) {
+    if (sp.first >= sp.last && !sp.end) continue;
+    hipEvent_t e0 = sp.first < sp.last ? pending[sp.first].a : sp.end;
+    hipEvent_t e1 = sp.end ? sp.end : pending[sp.last - 1].b;
+    float ms = 0.f;
+    MR_HIP(hipEventElapsedTime(&ms, e0, e1));
+    stats.phase_ms[sp.phase] += ms;
+    if (sp.end) ev_pool.push_back(sp.end);
+  }
+  for (auto& p : pending) {
     ev_pool.push_back(p.a);
     ev_pool.push_back(p.b);
   }
   pending.clear();
+  spans.clear();
   return 0;
 }
 
@@ -535,6 +558,7 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr) {
   const int mv_cls = user ? MR_K_MATVEC_USERS : MR_K_MATVEC_ITEMS;
   const int64_t n = S.E * ldk;
   const int64_t nb = user ? S.E : 0;
+  const size_t pend0 = pending.size();
   memset(h_init, 0, sizeof(CgState));
   h_init->min_dec = min_dec;
   h_init->max_it = max_it;
@@ -605,7 +629,7 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr) {
     while (known + 1 < (int)seq_of.size() && seq_of[known + 1] <= ms.seq) ++known;
     MR_CHECK(launched <= max_it + 2, "CG did not terminate");
   }
-  if (resolve_timing(ms.n_matvec)) return -1;
+  for (size_t i = pend0; i < pending.size(); ++i) pending[i].n_real = ms.n_matvec;
   if (final_rr) *final_rr = ms.final_rr;
   return ms.ret;
 }
@@ -631,13 +655,9 @@ int Engine::solve(Side& S) {
 int Engine::half_step(bool user, double min_dec, int max_it, double* final_rr) {
   MR_HIP(hipSetDevice(device));
   Side& S = user ? su : si;
-  hipEvent_t p0 = nullptr, p1 = nullptr, p2 = nullptr;
-  if (timing) {
-    if (ev_get(&p0) || ev_get(&p1) || ev_get(&p2)) return -1;
-    MR_HIP(hipEventRecord(p0, stream));
-  }
+  const size_t g0 = pending.size();
   if (gram(S)) return -1;
-  if (timing) MR_HIP(hipEventRecord(p1, stream));
+  const size_t c0 = pending.size();
   int its = 0;
   double rr = 0.0;
   if (solver == MR_SOLVER_CG) {
@@ -648,15 +668,14 @@ int Engine::half_step(bool user, double min_dec, int max_it, double* final_rr) {
   }
   if (allgather_side(user)) return -1;
   if (timing) {
-    MR_HIP(hipEventRecord(p2, stream));
-    MR_HIP(hipStreamSynchronize(stream));
-    float g = 0.f, s = 0.f;
-    MR_HIP(hipEventElapsedTime(&g, p0, p1));
-    MR_HIP(hipEventElapsedTime(&s, p1, p2));
-    stats.phase_ms[user ? 0 : 2] += g;
-    stats.phase_ms[user ? 1 : 3] += s;
-    ev_pool.push_back(p0); ev_pool.push_back(p1); ev_pool.push_back(p2);
-    if (resolve_timing(1 << 30)) return -1;
+    hipEvent_t end = nullptr;
+    if (sharded()) {   // the RCCL exchange belongs to the solve phase
+      if (ev_get(&end)) return -1;
+      MR_HIP(hipEventRecord(end, stream));
+    }
+    spans.push_back({user ? 0 : 2, g0, c0, nullptr});
+    spans.push_back({user ? 1 : 3, c0, pending.size(), end});
+    if (pending.size() > 8192 && resolve_timing()) return -1;
   }
   if (user) {
     stats.last_cg_users = its;

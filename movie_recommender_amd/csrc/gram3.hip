@@ -66,7 +66,7 @@ int launch_split_table(hipStream_t s, int64_t rows, int k, const float* F, uint1
   const int ldk = ldk_of(k);
   const int64_t n = rows * ldk;
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
-  split_table_kernel<<<grid, 256, 0, s>>>(rows, nb16_of(k), ldk, F, Fs);
+  MR_LAUNCH(split_table_kernel, grid, dim3(256), 0, s, rows, nb16_of(k), ldk, F, Fs);
   MR_HIP(hipGetLastError());
   return 0;
 }
@@ -323,7 +323,7 @@ int launch_gram3(hipStream_t s, bool user_side, int k, const WorkItem* work, int
   const int64_t grid = (n_work + 3) / 4;
   const int ldk = ldk_of(k);
 #define MR_G3(NB, U)                                                                 \
-  gram3_kernel<NB, U><<<dim3((unsigned)grid), dim3(256), 0, s>>>(work, n_work, idx, val, Fs, \
+  MR_LAUNCH((gram3_kernel<NB, U>), dim3((unsigned)grid), dim3(256), 0, s, work, n_work, idx, val, Fs, \
                                                                    bias, k, ldk, zrow, direct, slab)
   switch (nb16_of(k)) {
     case 2:

@@ -327,8 +327,8 @@ static int launch_gram_g(hipStream_t s, bool user_side, int k, const WorkItem* w
     nts = (e && atoi(e) == 1) ? 1 : 0;
   }
 #define MR_GRAM_LAUNCH(U, N)                                                  \
-  gram_kernel<NB, G, U, N><<<dim3((unsigned)grid), dim3(256), 0, s>>>(        \
-      work, n_work, idx, val, F, bias, k, ldk_of(k), zrow, direct, slab)
+  MR_LAUNCH((gram_kernel<NB, G, U, N>), dim3((unsigned)grid), dim3(256), 0, s, \
+            work, n_work, idx, val, F, bias, k, ldk_of(k), zrow, direct, slab)
   if (user_side) {
     if (nts) MR_GRAM_LAUNCH(true, true); else MR_GRAM_LAUNCH(true, false);
   } else {
@@ -437,9 +437,9 @@ int launch_slab_reduce(hipStream_t s, bool user_side, int k,
   const int64_t used4 = (gsize_of(k) + 2 * ldk + 2 + 3) / 4;
   const dim3 grid((unsigned)n_split, (unsigned)((used4 + 255) / 256));
   if (user_side)
-    slab_reduce_kernel<true><<<grid, dim3(256), 0, s>>>(split, slab, rec, k, ldk, direct);
+    MR_LAUNCH(slab_reduce_kernel<true>, grid, dim3(256), 0, s, split, slab, rec, k, ldk, direct);
   else
-    slab_reduce_kernel<false><<<grid, dim3(256), 0, s>>>(split, slab, rec, k, ldk, direct);
+    MR_LAUNCH(slab_reduce_kernel<false>, grid, dim3(256), 0, s, split, slab, rec, k, ldk, direct);
   MR_HIP(hipGetLastError());
   return 0;
 }
@@ -741,7 +741,7 @@ static int launch_matvec_nb(hipStream_t s, bool user_side, const CgState* st, in
                             int n_part, CgState* fst, int phase) {
   const bool nt = matvec_nt();
 #define MR_MV_LAUNCH(U, N)                                                          \
-  cg_matvec_kernel<NB, U, N><<<dim3(n_part), dim3(256), 0, s>>>(                    \
+  MR_LAUNCH((cg_matvec_kernel<NB, U, N>), dim3(n_part), dim3(256), 0, s,             \
       st, update_p, E, k, ldk_of(k), G, Gs, Gn, v, vb, r, rb, y, yb, partials, fst, phase)
   if (user_side) {
     if (nt) MR_MV_LAUNCH(true, true); else MR_MV_LAUNCH(true, false);
@@ -841,7 +841,7 @@ int launch_cg_update(hipStream_t s, const CgState* st, int mode, int64_t n,
                      const float* c, float* xb, float* rb, float* pb,
                      const float* qb, const float* cb, double* partials,
                      int n_part, CgState* fst, CgMirror* mirror, int seq) {
-  cg_update_kernel<<<dim3(n_part), dim3(256), 0, s>>>(
+  MR_LAUNCH(cg_update_kernel, dim3(n_part), dim3(256), 0, s,
       st, mode, n / 4, nb, x, r, p, q, c, xb, rb, pb, qb, cb, partials, fst, mirror, seq);
   MR_HIP(hipGetLastError());
   return 0;
@@ -875,7 +875,7 @@ __global__ __launch_bounds__(256) void cg_control_kernel(
 
 int launch_cg_control(hipStream_t s, CgState* st, int phase, int ctl,
                       const double* partials, int n_part, CgMirror* mirror, int seq) {
-  cg_control_kernel<<<dim3(1), dim3(256), 0, s>>>(st, phase, ctl, partials, n_part,
+  MR_LAUNCH(cg_control_kernel, dim3(1), dim3(256), 0, s, st, phase, ctl, partials, n_part,
                                                   mirror, seq);
   MR_HIP(hipGetLastError());
   return 0;
@@ -968,12 +968,12 @@ int launch_solve(hipStream_t s, bool user_side, int64_t E, int k, double ridge,
   if (user_side) {
     MR_HIP(hipFuncSetAttribute((const void*)solve_kernel<true>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    solve_kernel<true><<<dim3((unsigned)E), dim3(256), lds, s>>>(
+    MR_LAUNCH(solve_kernel<true>, dim3((unsigned)E), dim3(256), lds, s,
         E, k, ldk_of(k), ridge, G, Gs, Gn, C, Cb, x, xb, nonpd);
   } else {
     MR_HIP(hipFuncSetAttribute((const void*)solve_kernel<false>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    solve_kernel<false><<<dim3((unsigned)E), dim3(256), lds, s>>>(
+    MR_LAUNCH(solve_kernel<false>, dim3((unsigned)E), dim3(256), lds, s,
         E, k, ldk_of(k), ridge, G, Gs, Gn, C, Cb, x, xb, nonpd);
   }
   MR_HIP(hipGetLastError());

@@ -2,10 +2,30 @@
 // Target: MI355X (gfx950, CDNA4) only.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <string>
 
 namespace mr {
+
+// Per-thread launch-timing slot, set by the engine around a timed launcher
+// (Engine::tic/toc).  Kernels launched through MR_LAUNCH record the slot's
+// events from their own dispatch packets (hipExtLaunchKernel): the first
+// launch takes the start event, every launch the stop event.  No marker
+// packets go between kernels, so timing does not add gaps to the stream.
+struct LaunchTiming {
+  hipEvent_t start = nullptr;
+  hipEvent_t stop = nullptr;
+};
+extern thread_local LaunchTiming t_launch;
+
+#define MR_LAUNCH(kernel, grid, block, shm, s, ...)                                  \
+  do {                                                                               \
+    hipEvent_t mr_ev0_ = ::mr::t_launch.start;                                       \
+    ::mr::t_launch.start = nullptr;                                                  \
+    hipExtLaunchKernelGGL(kernel, grid, block, shm, s, mr_ev0_, ::mr::t_launch.stop, \
+                          0, __VA_ARGS__);                                           \
+  } while (0)
 
 // Error handling --------------------------------------------------------------
 void set_error(const std::string& msg);
