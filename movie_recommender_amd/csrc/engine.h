@@ -94,7 +94,7 @@ struct Engine {
   int set_rccl(const unsigned char* id, int rank, int world);
   int allreduce_state_slot();
   int allgather_side(bool user);
-  int control(int phase, int seq);
+  int finalize_sharded(int phase, int seq);
   int wait_mirror(int target, CgMirror* out);
   GramDst direct_dst(Side& S);
   GramDst slab_dst(Side& S);

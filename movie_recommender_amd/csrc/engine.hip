@@ -445,19 +445,14 @@ int Engine::allgather_side(bool user) {
   return 0;
 }
 
-int Engine::control(int phase, int seq) {
+// Sharded CG: all-reduce the slot the last block filled, then apply the rule.
+int Engine::finalize_sharded(int phase, int seq) {
+  if (allreduce_state_slot()) return -1;
   hipEvent_t a = nullptr;
   if (tic(MR_K_CG_CONTROL, -1, &a)) return -1;
-  CgMirror* m = seq > 0 ? d_mirror : nullptr;
-  if (!sharded()) {
-    if (launch_cg_control(stream, d_state, phase, CTL_BOTH, partials, cur_parts, m, seq))
-      return -1;
-  } else {
-    if (launch_cg_control(stream, d_state, phase, CTL_REDUCE, partials, cur_parts)) return -1;
-    if (allreduce_state_slot()) return -1;
-    if (launch_cg_control(stream, d_state, phase, CTL_FINALIZE, partials, cur_parts, m, seq))
-      return -1;
-  }
+  if (launch_cg_control(stream, d_state, phase, CTL_FINALIZE, partials, cur_parts,
+                        seq > 0 ? d_mirror : nullptr, seq))
+    return -1;
   return toc(MR_K_CG_CONTROL, -1, a);
 }
 
@@ -562,13 +557,16 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr) {
   memset(h_init, 0, sizeof(CgState));
   h_init->min_dec = min_dec;
   h_init->max_it = max_it;
+  h_init->sharded = sharded() ? 1 : 0;
   MR_HIP(hipMemcpyAsync(d_state, h_init, sizeof(CgState), hipMemcpyHostToDevice, stream));
-  // Single-GPU runs fold the control steps into the last block of the matvec
-  // (alpha) and of the update (INIT / BETA rules + publish): two kernels per
-  // iteration instead of four.  Sharded runs keep the control kernels, whose
-  // reduce and finalize halves bracket the RCCL all-reduce.
-  const bool fused = !sharded();
-  CgState* fst = fused ? d_state : nullptr;
+  // The control steps run in the last-arriving block of the matvec (alpha)
+  // and of the update (INIT / BETA rules + publish): two kernels per
+  // iteration.  Sharded runs: those blocks only sum the local partials into
+  // the state slot, RCCL all-reduces it, the update derives alpha from the
+  // reduced slot itself, and a one-block finalize applies the INIT / BETA
+  // rules -- three kernels and two all-reduces per iteration.
+  const bool shard = sharded();
+  CgState* fst = d_state;
   // r0 = G x - c ; p0 = -r0 ; rr  (matrix.cpp:464-485)
   hipEvent_t a = nullptr;
   if (tic(mv_cls, -1, &a)) return -1;
@@ -583,7 +581,7 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr) {
     return -1;
   if (toc(MR_K_CG_UPDATE, -1, a)) return -1;
   cur_parts = kUpdParts;
-  if (!fused && control(CG_INIT, seq_init)) return -1;
+  if (shard && finalize_sharded(CG_INIT, seq_init)) return -1;
 
   std::vector<int> seq_of;   // publish seq of iteration t's BETA step
   auto launch_iter = [&](int t) -> int {
@@ -594,7 +592,7 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr) {
       return -1;
     if (toc(mv_cls, t, ev)) return -1;
     cur_parts = S.n_part_mv;
-    if (!fused && control(CG_ALPHA, 0)) return -1;
+    if (shard && allreduce_state_slot()) return -1;
     seq_of.push_back(++mirror_seq);
     if (tic(MR_K_CG_UPDATE, t, &ev)) return -1;
     if (launch_cg_update(stream, d_state, UPD_STEP, n, nb, xf, S.r, S.p, S.q, S.C, xb, S.rb,
@@ -602,7 +600,7 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr) {
       return -1;
     if (toc(MR_K_CG_UPDATE, t, ev)) return -1;
     cur_parts = kUpdParts;
-    return fused ? 0 : control(CG_BETA, seq_of.back());
+    return shard ? finalize_sharded(CG_BETA, seq_of.back()) : 0;
   };
 
   // Iteration 0 cannot stop by stagnation (fails starts at 0) and iteration 1

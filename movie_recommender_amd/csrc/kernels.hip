@@ -531,7 +531,14 @@ __device__ void last_block_finalize(CgState* st, int phase, double* partials, Cg
   const double tot = block_sum_f64<256>(acc, sh);
   if (threadIdx.x == 0) {
     __hip_atomic_store(&st->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    cg_finalize(st, phase, tot, mirror, seq);
+    if (st->sharded) {
+      // local sum for the all-reduce; the update computes alpha itself from
+      // the reduced slot, so ALPHA needs no finalize step (only its count)
+      st->comm[0] = tot;
+      if (phase == CG_BETA) st->n_matvec += 1;
+    } else {
+      cg_finalize(st, phase, tot, mirror, seq);
+    }
   }
 }
 
@@ -784,7 +791,9 @@ __global__ __launch_bounds__(256) void cg_update_kernel(
     double* __restrict__ partials, CgState* fst, CgMirror* mirror, int seq) {
   if (st->done) return;
   __shared__ double sh[4];
-  const float alpha = (float)st->alpha;
+  // sharded runs: alpha = rr / (all-reduced p.Ap), the ALPHA rule inline
+  const float alpha =
+      (float)(st->sharded && mode != UPD_INIT ? st->rr / st->comm[0] : st->alpha);
   double acc = 0.0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

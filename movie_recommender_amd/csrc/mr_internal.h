@@ -144,7 +144,7 @@ struct CgState {
   int32_t max_it;
   int32_t n_matvec; // matvec launches that did work (for kernel timing)
   uint32_t arrive;  // blocks finished (fused control: the last one finalizes)
-  uint32_t pad;
+  int32_t sharded;  // 1: the last block only sums into comm[0] for the all-reduce
 };
 
 // Host-visible copy of the CG state, written by cg_control into pinned,
