@@ -196,6 +196,9 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    # snapshot of the iterate: the event-free pass below replays the SAME
+    # steps (bit-identical kernels, so identical CG iteration counts)
+    snap = ctx.get_factors() if not args.no_kernel_events else None
     barrier()
     t_start = time.perf_counter()
     for s in range(args.steps):
@@ -209,10 +212,12 @@ def main():
         elapsed = float(tt.item())
     st = ctx.stats()
     ctx.set_timing(False)
-    # The same K steps again without per-launch events (informational: the
-    # event timestamps of hipExtLaunchKernel cost a few us per launch).
+    # The same K steps again without per-launch events, replayed from the
+    # snapshot (informational: the event timestamps of hipExtLaunchKernel
+    # cost a few us per launch).
     plain_ms = None
     if not args.no_kernel_events:
+        ctx.set_factors(*snap)
         barrier()
         t1 = time.perf_counter()
         for s in range(args.steps):

@@ -47,6 +47,7 @@ enum {
   MR_K_CG_UPDATE,        /* CG x/r update + r.r partials (both sides)         */
   MR_K_CG_CONTROL,       /* CG scalar reduction / stop rule (both sides)      */
   MR_K_SOLVE,            /* batched Cholesky (exact mode)                      */
+  MR_K_CG_START,         /* CG start of split entities (fused start)          */
   MR_K_COUNT
 };
 

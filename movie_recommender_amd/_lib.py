@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MR_LIB_PATH") or os.path.join(HERE, "lib", "cpp_ls_lib.so")
 
 K_NAMES = ["gram_users", "gram_items", "slab_reduce", "matvec_users",
-           "matvec_items", "cg_update", "cg_control", "solve"]
+           "matvec_items", "cg_update", "cg_control", "solve", "cg_start_split"]
 
 
 class MrStats(ctypes.Structure):

@@ -29,6 +29,8 @@ struct Side {
   float *r = nullptr, *p = nullptr, *q = nullptr;
   float *rb = nullptr, *pb = nullptr, *qb = nullptr;
   int n_part_mv = 1;
+  double* start_parts = nullptr;   // fused CG start: (r.r, p.Gp) per block
+  int64_t n_start_pairs = 0;
 };
 
 struct Pending {
@@ -67,6 +69,7 @@ struct Engine {
   int solver = MR_SOLVER_CG;
   double ridge = 0.0;
   int chunk = 2048;
+  bool fuse_start = true;   // CG start in the Gram epilogue (MR_FUSE_START=0: off)
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
   std::vector<Pending> pending;
@@ -92,15 +95,16 @@ struct Engine {
   // single-rank) or host callbacks with more than one rank.
   bool sharded() const { return rccl != nullptr || (has_comm && comm.world > 1); }
   int set_rccl(const unsigned char* id, int rank, int world);
-  int allreduce_state_slot();
+  int allreduce_state_slot(int count = 1);
   int allgather_side(bool user);
   int finalize_sharded(int phase, int seq);
   int wait_mirror(int target, CgMirror* out);
   GramDst direct_dst(Side& S);
   GramDst slab_dst(Side& S);
-  int gram(Side& S);
+  int gram(Side& S, bool start = false);
   int x_ptrs(Side& S, float** xf, float** xb);
-  int cg(Side& S, double min_dec, int max_it, double* final_rr);
+  int cg(Side& S, double min_dec, int max_it, double* final_rr, bool started = false);
+  CgStart cg_start_of(Side& S);
   int solve(Side& S);
   int half_step(bool user, double min_dec, int max_it, double* final_rr);
   int run(double min_dec, int max_it);

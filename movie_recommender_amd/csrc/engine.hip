@@ -50,6 +50,7 @@ static void free_side(Side& S, hipStream_t s) {
   dfree(S.G, s); dfree(S.Gs, s); dfree(S.Gn, s); dfree(S.C, s); dfree(S.Cb, s);
   dfree(S.r, s); dfree(S.p, s); dfree(S.q, s);
   dfree(S.rb, s); dfree(S.pb, s); dfree(S.qb, s);
+  dfree(S.start_parts, s);
 }
 
 Engine::~Engine() {
@@ -212,6 +213,9 @@ int Engine::build_side(Side& S, bool user, int64_t n, const int32_t* d_key,
   MR_HIP(hipMemsetAsync(S.r, 0, ef * sizeof(float), stream));
   MR_HIP(hipMemsetAsync(S.p, 0, ef * sizeof(float), stream));
   MR_HIP(hipMemsetAsync(S.q, 0, ef * sizeof(float), stream));
+  // fused CG start: one (r.r, p.Gp) pair per Gram block, then per split block
+  S.n_start_pairs = gram_blocks(S.n_work) + (S.n_split + 3) / 4;
+  if (dalloc(&S.start_parts, 2 * std::max<int64_t>(1, S.n_start_pairs), stream)) return -1;
   // matvec grid: one wave per entity, fixed grid for reproducible partials
   int64_t g = (S.E + 3) / 4;
   S.n_part_mv = (int)std::max<int64_t>(1, std::min<int64_t>(g, kMaxParts));
@@ -262,6 +266,8 @@ int Engine::init(int dev, int k_, int64_t U_, int64_t I_, int64_t n_u,
   {
     const char* e = getenv("MR_GRAM3");
     use_gram3 = gram3_supported(k) && e && atoi(e) == 1;
+    const char* f = getenv("MR_FUSE_START");
+    fuse_start = !(f && atoi(f) == 0);
   }
   if (use_gram3 && dalloc(&Fsplit, (std::max(U, I) + 1) * 3 * ldk, stream)) return -1;
   // upload + build both views
@@ -379,19 +385,19 @@ int Engine::set_rccl(const unsigned char* id, int rank, int world) {
 
 // Sum the CG scalar slot over ranks.  RCCL: in place on the device, ordered on
 // the engine stream (no host synchronisation).  Callbacks: staged via host.
-int Engine::allreduce_state_slot() {
+int Engine::allreduce_state_slot(int count) {
   if (!sharded()) return 0;
   if (rccl) {
-    MR_NCCL(ncclAllReduce(&d_state->comm[0], &d_state->comm[0], 1, ncclDouble, ncclSum,
-                          (ncclComm_t)rccl, stream));
+    MR_NCCL(ncclAllReduce(&d_state->comm[0], &d_state->comm[0], (size_t)count, ncclDouble,
+                          ncclSum, (ncclComm_t)rccl, stream));
     return 0;
   }
-  MR_HIP(hipMemcpyAsync(h_stage, &d_state->comm[0], sizeof(double),
+  MR_HIP(hipMemcpyAsync(h_stage, &d_state->comm[0], count * sizeof(double),
                         hipMemcpyDeviceToHost, stream));
   MR_HIP(hipStreamSynchronize(stream));
-  MR_CHECK(comm.allreduce_f64(comm.user, (double*)h_stage, 1) == 0,
+  MR_CHECK(comm.allreduce_f64(comm.user, (double*)h_stage, count) == 0,
            "allreduce callback failed");
-  MR_HIP(hipMemcpyAsync(&d_state->comm[0], h_stage, sizeof(double),
+  MR_HIP(hipMemcpyAsync(&d_state->comm[0], h_stage, count * sizeof(double),
                         hipMemcpyHostToDevice, stream));
   return 0;
 }
@@ -502,7 +508,20 @@ GramDst Engine::slab_dst(Side& S) {
   return d;
 }
 
-int Engine::gram(Side& S) {
+CgStart Engine::cg_start_of(Side& S) {
+  CgStart cs{};
+  float *xf, *xb;
+  x_ptrs(S, &xf, &xb);
+  cs.x = xf;
+  cs.xb = xb;
+  cs.r = S.r; cs.rb = S.rb; cs.p = S.p; cs.pb = S.pb; cs.q = S.q; cs.qb = S.qb;
+  cs.parts = S.start_parts;
+  return cs;
+}
+
+// start: the Gram waves also start the CG solve (r0, p0, q0 = G p0 and the
+// block pairs of r.r / p.Gp); Engine::cg(started = true) finishes the start.
+int Engine::gram(Side& S, bool start) {
   const bool user = S.user;
   const float* F = user ? Vfac : Ufac;
   const float* bias = user ? nullptr : Ubias;
@@ -515,9 +534,11 @@ int Engine::gram(Side& S) {
         launch_gram3(stream, user, k, S.work, S.n_work, S.idx, S.val, Fsplit, bias, zrow,
                      direct_dst(S), slab_dst(S)))
       return -1;
-  } else if (launch_gram(stream, user, k, S.work, S.n_work, S.idx, S.val, F, bias, zrow,
-                         direct_dst(S), slab_dst(S))) {
-    return -1;
+  } else {
+    const CgStart cs = cg_start_of(S);
+    if (launch_gram(stream, user, k, S.work, S.n_work, S.idx, S.val, F, bias, zrow,
+                    direct_dst(S), slab_dst(S), start ? &cs : nullptr))
+      return -1;
   }
   if (toc(cls, -1, a)) return -1;
   if (S.n_split) {
@@ -546,7 +567,7 @@ int Engine::x_ptrs(Side& S, float** xf, float** xb) {
 // iteration t's state is known only when the known state (after t-1) proves
 // that t cannot terminate (fails == 0, rr far above 1e-6, t+1 < max_it) --
 // so the stream stays busy without launching iterations that would be idle.
-int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr) {
+int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr, bool started) {
   float *xf, *xb;
   x_ptrs(S, &xf, &xb);
   const bool user = S.user;
@@ -558,7 +579,6 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr) {
   h_init->min_dec = min_dec;
   h_init->max_it = max_it;
   h_init->sharded = sharded() ? 1 : 0;
-  MR_HIP(hipMemcpyAsync(d_state, h_init, sizeof(CgState), hipMemcpyHostToDevice, stream));
   // The control steps run in the last-arriving block of the matvec (alpha)
   // and of the update (INIT / BETA rules + publish): two kernels per
   // iteration.  Sharded runs: those blocks only sum the local partials into
@@ -567,32 +587,62 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr) {
   // rules -- three kernels and two all-reduces per iteration.
   const bool shard = sharded();
   CgState* fst = d_state;
-  // r0 = G x - c ; p0 = -r0 ; rr  (matrix.cpp:464-485)
   hipEvent_t a = nullptr;
-  if (tic(mv_cls, -1, &a)) return -1;
-  if (launch_cg_matvec(stream, user, d_state, 0, S.E, k, S.G, S.Gs, S.Gn, xf, xb,
-                       S.r, S.rb, S.q, S.qb, partials, S.n_part_mv))
-    return -1;
-  if (toc(mv_cls, -1, a)) return -1;
   const int seq_init = ++mirror_seq;
-  if (tic(MR_K_CG_UPDATE, -1, &a)) return -1;
-  if (launch_cg_update(stream, d_state, UPD_INIT, n, nb, xf, S.r, S.p, S.q, S.C, xb,
-                       S.rb, S.pb, S.qb, S.Cb, partials, kUpdParts, fst, d_mirror, seq_init))
-    return -1;
-  if (toc(MR_K_CG_UPDATE, -1, a)) return -1;
-  cur_parts = kUpdParts;
-  if (shard && finalize_sharded(CG_INIT, seq_init)) return -1;
+  if (started) {
+    // The Gram waves already formed r0, p0 = -r0 and q0 = G p0 with block
+    // pairs of (r0.r0, p0.q0); split entities follow here, then one control
+    // block applies the INIT rule and alpha of iteration 0 (CG_START).
+    if (S.n_split) {
+      const CgStart cs = cg_start_of(S);
+      if (tic(MR_K_CG_START, -1, &a)) return -1;
+      if (launch_cg_start_split(stream, user, k, S.split, S.n_split, direct_dst(S), cs,
+                                S.start_parts + 2 * gram_blocks(S.n_work)))
+        return -1;
+      if (toc(MR_K_CG_START, -1, a)) return -1;
+    }
+    const int np = (int)S.n_start_pairs;
+    if (tic(MR_K_CG_CONTROL, -1, &a)) return -1;
+    if (shard) {
+      if (launch_cg_control(stream, d_state, CG_START, CTL_REDUCE, S.start_parts, np) ||
+          allreduce_state_slot(2) ||
+          launch_cg_control(stream, d_state, CG_START, CTL_FINALIZE, S.start_parts, np,
+                            d_mirror, seq_init, min_dec, max_it, 1))
+        return -1;
+    } else if (launch_cg_control(stream, d_state, CG_START, CTL_BOTH, S.start_parts, np,
+                                 d_mirror, seq_init, min_dec, max_it, 0)) {
+      return -1;
+    }
+    if (toc(MR_K_CG_CONTROL, -1, a)) return -1;
+  } else {
+    MR_HIP(hipMemcpyAsync(d_state, h_init, sizeof(CgState), hipMemcpyHostToDevice, stream));
+    // r0 = G x - c ; p0 = -r0 ; rr  (matrix.cpp:464-485)
+    if (tic(mv_cls, -1, &a)) return -1;
+    if (launch_cg_matvec(stream, user, d_state, 0, S.E, k, S.G, S.Gs, S.Gn, xf, xb,
+                         S.r, S.rb, S.q, S.qb, partials, S.n_part_mv))
+      return -1;
+    if (toc(mv_cls, -1, a)) return -1;
+    if (tic(MR_K_CG_UPDATE, -1, &a)) return -1;
+    if (launch_cg_update(stream, d_state, UPD_INIT, n, nb, xf, S.r, S.p, S.q, S.C, xb,
+                         S.rb, S.pb, S.qb, S.Cb, partials, kUpdParts, fst, d_mirror, seq_init))
+      return -1;
+    if (toc(MR_K_CG_UPDATE, -1, a)) return -1;
+    cur_parts = kUpdParts;
+    if (shard && finalize_sharded(CG_INIT, seq_init)) return -1;
+  }
 
   std::vector<int> seq_of;   // publish seq of iteration t's BETA step
   auto launch_iter = [&](int t) -> int {
     hipEvent_t ev = nullptr;
-    if (tic(mv_cls, t, &ev)) return -1;
-    if (launch_cg_matvec(stream, user, d_state, t > 0, S.E, k, S.G, S.Gs, S.Gn, S.p, S.pb,
-                         S.r, S.rb, S.q, S.qb, partials, S.n_part_mv, fst, CG_ALPHA))
-      return -1;
-    if (toc(mv_cls, t, ev)) return -1;
-    cur_parts = S.n_part_mv;
-    if (shard && allreduce_state_slot()) return -1;
+    if (!(started && t == 0)) {   // a fused start has done iteration 0's matvec
+      if (tic(mv_cls, t, &ev)) return -1;
+      if (launch_cg_matvec(stream, user, d_state, t > 0, S.E, k, S.G, S.Gs, S.Gn, S.p, S.pb,
+                           S.r, S.rb, S.q, S.qb, partials, S.n_part_mv, fst, CG_ALPHA))
+        return -1;
+      if (toc(mv_cls, t, ev)) return -1;
+      cur_parts = S.n_part_mv;
+      if (shard && allreduce_state_slot()) return -1;
+    }
     seq_of.push_back(++mirror_seq);
     if (tic(MR_K_CG_UPDATE, t, &ev)) return -1;
     if (launch_cg_update(stream, d_state, UPD_STEP, n, nb, xf, S.r, S.p, S.q, S.C, xb, S.rb,
@@ -654,12 +704,13 @@ int Engine::half_step(bool user, double min_dec, int max_it, double* final_rr) {
   MR_HIP(hipSetDevice(device));
   Side& S = user ? su : si;
   const size_t g0 = pending.size();
-  if (gram(S)) return -1;
+  const bool fused = solver == MR_SOLVER_CG && fuse_start && !use_gram3;
+  if (gram(S, fused)) return -1;
   const size_t c0 = pending.size();
   int its = 0;
   double rr = 0.0;
   if (solver == MR_SOLVER_CG) {
-    its = cg(S, min_dec, max_it, &rr);
+    its = cg(S, min_dec, max_it, &rr, fused);
     if (its < 0) return -1;
   } else {
     if (solve(S)) return -1;

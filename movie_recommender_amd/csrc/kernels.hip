@@ -20,6 +20,7 @@
 namespace mr {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------
 // helpers
@@ -50,6 +51,446 @@ __device__ __forceinline__ double block_sum_f64(double v, double* sh) {
   return t;  // valid on thread 0
 }
 
+constexpr int MV_WAVES = 4;
+constexpr int MV_CST = 68;   // float4 stride of a column-partial row (+16 floats: no bank clash)
+
+// Per-wave LDS scratch of the tile GEMV (one entity at a time).
+template <int NB>
+struct MvScratch {
+  static constexpr int NF = NB / 2;
+  float pv[16 * NB];               // the vector, virtual order
+  float redR[NB][64];              // 4-lane row partials
+  float4 redC[NB][MV_CST];         // 16-lane column partials
+  float dd[NF > 0 ? 16 * NF : 1];  // side-array diagonals of the folded tiles
+};
+
+// y = G_e v for ONE entity, by one wave, on tri16 tiles already in registers
+// (lane l holds float4 l of every tile: T[l>>2][4(l&3) .. +3]).  Lane l
+// accumulates the row product T v_bj into y_bi and, for bi < bj, the column
+// product T^T v_bi into y_bj; the 4-lane row partials and 16-lane column
+// partials are combined through LDS in a fixed order.  Requires sc.pv (v in
+// virtual order) and sc.dd staged.  Returns y at virtual index lane + 64 h in
+// yo[h] (0 for padding, n >= k) and, user side, the bias row
+// yb = Gs.v + Gn vb (wave-uniform); Gs_e / gn are the entity's row sums and
+// count.  The user-side bias column Gs vb is added to every y.
+template <int NB, bool USER>
+__device__ __forceinline__ void tile_matvec(
+    const float4 (&g)[NB * (NB - 1) / 2 + NB / 2 + (NB & 1)], MvScratch<NB>& sc, float vb,
+    const float* __restrict__ Gs_e, float gn, int k, float (&yo)[(16 * NB + 63) / 64],
+    float& yb) {
+  constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2;
+  constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
+  const int lane = threadIdx.x & 63;
+  const int rr = lane >> 2, c4 = (lane & 3) * 4;
+  float accR[NB];
+  float4 accC[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    accR[b] = 0.f;
+    accC[b] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  // strictly-upper tiles: row product into y_bi, column product into y_bj
+  int t = 0;
+#pragma unroll
+  for (int bi = 0; bi < NB; ++bi) {
+    const float pi = sc.pv[16 * bi + rr];
+#pragma unroll
+    for (int bj = bi + 1; bj < NB; ++bj) {
+      const float4 gg = g[t];
+      const float4 pj = *reinterpret_cast<const float4*>(&sc.pv[16 * bj + c4]);
+      float s0 = accR[bi];
+      s0 = fmaf(gg.x, pj.x, s0);
+      s0 = fmaf(gg.y, pj.y, s0);
+      s0 = fmaf(gg.z, pj.z, s0);
+      s0 = fmaf(gg.w, pj.w, s0);
+      accR[bi] = s0;
+      accC[bj].x = fmaf(gg.x, pi, accC[bj].x);
+      accC[bj].y = fmaf(gg.y, pi, accC[bj].y);
+      accC[bj].z = fmaf(gg.z, pi, accC[bj].z);
+      accC[bj].w = fmaf(gg.w, pi, accC[bj].w);
+      ++t;
+    }
+  }
+  // folded diagonal tiles: c >= r belongs to D_2m (row; column also for
+  // c > r), c < r to D_2m+1 (row and column)
+#pragma unroll
+  for (int m = 0; m < NF; ++m) {
+    const int b0 = 2 * m, b1 = 2 * m + 1;
+    const float4 gg = g[NO + m];
+    const float ge[4] = {gg.x, gg.y, gg.z, gg.w};
+    const float4 p0 = *reinterpret_cast<const float4*>(&sc.pv[16 * b0 + c4]);
+    const float4 p1 = *reinterpret_cast<const float4*>(&sc.pv[16 * b1 + c4]);
+    const float p0c[4] = {p0.x, p0.y, p0.z, p0.w};
+    const float p1c[4] = {p1.x, p1.y, p1.z, p1.w};
+    const float pr0 = sc.pv[16 * b0 + rr], pr1 = sc.pv[16 * b1 + rr];
+    float c0[4], c1[4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const int c = c4 + x;
+      const float gu = (c >= rr) ? ge[x] : 0.f;
+      const float gc = (c > rr) ? ge[x] : 0.f;
+      const float gl = (c < rr) ? ge[x] : 0.f;
+      accR[b0] = fmaf(gu, p0c[x], accR[b0]);
+      accR[b1] = fmaf(gl, p1c[x], accR[b1]);
+      c0[x] = gc * pr0;
+      c1[x] = gl * pr1;
+    }
+    accC[b0].x += c0[0]; accC[b0].y += c0[1]; accC[b0].z += c0[2]; accC[b0].w += c0[3];
+    accC[b1].x += c1[0]; accC[b1].y += c1[1]; accC[b1].z += c1[2]; accC[b1].w += c1[3];
+  }
+  if constexpr ((NB & 1) != 0) {   // last diagonal block stored full: row product
+    const float4 gg = g[NO + NF];
+    const float4 pj = *reinterpret_cast<const float4*>(&sc.pv[16 * (NB - 1) + c4]);
+    float s0 = accR[NB - 1];
+    s0 = fmaf(gg.x, pj.x, s0);
+    s0 = fmaf(gg.y, pj.y, s0);
+    s0 = fmaf(gg.z, pj.z, s0);
+    s0 = fmaf(gg.w, pj.w, s0);
+    accR[NB - 1] = s0;
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    sc.redR[b][lane] = accR[b];
+    sc.redC[b][lane] = accC[b];
+  }
+  __builtin_amdgcn_wave_barrier();
+  float ybp = 0.f;
+#pragma unroll
+  for (int h = 0; h < NV; ++h) {
+    const int o = lane + 64 * h;   // virtual index
+    yo[h] = 0.f;
+    if (o >= NP) continue;
+    const int n = nat_of(o, NB);
+    if (n >= k) continue;
+    const int b = o >> 4, ii = o & 15;
+    const float* R = &sc.redR[b][4 * ii];
+    float y = (R[0] + R[1]) + (R[2] + R[3]);
+    const float* C = reinterpret_cast<const float*>(&sc.redC[b][0]) + ii;
+    float s = 0.f;
+#pragma unroll
+    for (int qq = 0; qq < 16; ++qq) s += C[16 * qq];
+    y += s;
+    if (NF > 0 && (b & 1) && b < 2 * NF) y = fmaf(sc.dd[(b >> 1) * 16 + ii], sc.pv[o], y);
+    if (USER) {
+      const float gs = Gs_e[n];
+      y = fmaf(gs, vb, y);
+      ybp = fmaf(gs, sc.pv[o], ybp);
+    }
+    yo[h] = y;
+  }
+  if (USER) yb = fmaf(gn, vb, wave_sum_f32(ybp));
+}
+
+// CG start for ONE entity, by one wave, in block form (cg_least_squares,
+// matrix.cpp:464-476 and the first matvec / dot of its loop, :493-497):
+//   r0 = G x - c,  p0 = -r0,  q0 = G p0
+// written to the CG vectors; this wave's lanes add r0.r0 to drr and p0.q0 to
+// dpq (fp64; callers reduce in a fixed order).  G / Gs / Gn / C / Cb hold the
+// entity's finished normal equations (read back through L2 right after the
+// Gram wave stored them, or after slab_reduce for split entities).
+template <int NB, bool USER>
+__device__ __forceinline__ void cg_start_entity(int64_t e, int k, int ldk,
+                                                const GramDst& D, const CgStart& cs,
+                                                MvScratch<NB>& sc, double& drr, double& dpq) {
+  constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2, NTILE = NO + NF + (NB & 1);
+  constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
+  const int lane = threadIdx.x & 63;
+  // x in natural order (staged to LDS in virtual order); c at the natural
+  // column of this lane's y slot h (virtual index lane + 64 h)
+  float xv[NV], cn[NV];
+#pragma unroll
+  for (int h = 0; h < NV; ++h) {
+    const int i = lane + 64 * h;
+    xv[h] = (i < NP) ? cs.x[e * ldk + i] : 0.f;
+    cn[h] = (i < NP) ? D.C[e * D.sV + nat_of(i, NB)] : 0.f;
+  }
+  const float xb = USER ? cs.xb[e] : 0.f;
+  const float cb = USER ? D.Cb[e * D.sS] : 0.f;
+  const float gn = USER ? D.Gn[e * D.sS] : 0.f;
+  const float* Gs_e = USER ? D.Gs + e * D.sV : nullptr;
+  const float4* __restrict__ Ge = reinterpret_cast<const float4*>(D.G + e * D.sG);
+  float4 g[NTILE];
+#pragma unroll
+  for (int t = 0; t < NTILE; ++t) g[t] = Ge[t * 64 + lane];
+  if (NF > 0 && lane < 16 * NF) sc.dd[lane] = D.G[e * D.sG + NTILE * 256 + lane];
+#pragma unroll
+  for (int h = 0; h < NV; ++h) {
+    const int i = lane + 64 * h;
+    if (i < NP) sc.pv[virt_of(i, NB)] = xv[h];
+  }
+  __builtin_amdgcn_wave_barrier();
+  float yo[NV], yb = 0.f;
+  tile_matvec<NB, USER>(g, sc, xb, Gs_e, gn, k, yo, yb);
+  __builtin_amdgcn_wave_barrier();
+  // r0 = G x - c, p0 = -r0 (:468-476); p0 replaces x in LDS
+  double d = 0.0;
+#pragma unroll
+  for (int h = 0; h < NV; ++h) {
+    const int o = lane + 64 * h;
+    if (o < NP) {
+      const int n = nat_of(o, NB);
+      float pn = 0.f;
+      if (n < k) {
+        const float rv = yo[h] - cn[h];
+        cs.r[e * ldk + n] = rv;
+        cs.p[e * ldk + n] = -rv;
+        d += (double)rv * rv;
+        pn = -rv;
+      }
+      sc.pv[o] = pn;
+    }
+  }
+  float pb = 0.f;
+  if (USER) {
+    const float rbv = yb - cb;
+    pb = -rbv;
+    if (lane == 0) {
+      cs.rb[e] = rbv;
+      cs.pb[e] = pb;
+      d += (double)rbv * rbv;
+    }
+  }
+  drr += wave_sum_f64(d);
+  __builtin_amdgcn_wave_barrier();
+  // q0 = G p0 and p0.q0 (:493-497)
+  tile_matvec<NB, USER>(g, sc, pb, Gs_e, gn, k, yo, yb);
+  d = 0.0;
+#pragma unroll
+  for (int h = 0; h < NV; ++h) {
+    const int o = lane + 64 * h;
+    if (o < NP) {
+      const int n = nat_of(o, NB);
+      if (n < k) {
+        cs.q[e * ldk + n] = yo[h];
+        d += (double)yo[h] * sc.pv[o];
+      }
+    }
+  }
+  if (USER && lane == 0) {
+    cs.qb[e] = yb;
+    d += (double)yb * pb;
+  }
+  dpq += wave_sum_f64(d);
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Fixed-order (r.r, p.Gp) pair per block: wave partials summed in wave order.
+__device__ __forceinline__ void store_start_pair(double drr, double dpq, double* parts) {
+  __shared__ double shp[4][2];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    shp[wid][0] = drr;
+    shp[wid][1] = dpq;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0.0, b = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+      a += shp[w][0];
+      b += shp[w][1];
+    }
+    parts[2 * (int64_t)blockIdx.x] = a;
+    parts[2 * (int64_t)blockIdx.x + 1] = b;
+  }
+}
+
+// NB contiguous floats at p (16-B aligned when NB % 4 == 0).
+template <int NB>
+__device__ __forceinline__ void load_row_seg(float (&v)[NB], const float* __restrict__ p) {
+  if constexpr (NB % 4 == 0) {
+#pragma unroll
+    for (int h = 0; h < NB / 4; ++h) {
+      const float4 t = reinterpret_cast<const float4*>(p)[h];
+      v[4 * h] = t.x; v[4 * h + 1] = t.y; v[4 * h + 2] = t.z; v[4 * h + 3] = t.w;
+    }
+  } else if constexpr (NB % 2 == 0) {
+#pragma unroll
+    for (int h = 0; h < NB / 2; ++h) {
+      const float2 t = reinterpret_cast<const float2*>(p)[h];
+      v[2 * h] = t.x; v[2 * h + 1] = t.y;
+    }
+  } else {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) v[b] = p[b];
+  }
+}
+
+// Per-wave LDS of the accumulator-based CG start (start_from_acc).
+constexpr int SR_STRIDE = 68;   // row-partial stride (floats): 4 r-rows hit distinct banks
+template <int NB>
+struct StartScratch {
+  float pv[16 * NB];                 // the vector, virtual order
+  float sC[16 * NB];                 // rhs c, virtual order
+  float sGs[16 * NB];                // user side: row sums, virtual order
+  float partR[NB * 4][SR_STRIDE];    // [4 bi + r][lane]: row-product partials
+  float partC[NB][64];               // [bj][lane]: column-product partials
+};
+
+// y = G v straight from the MFMA accumulators of the Gram wave (no memory
+// round trip).  acc[t(bi,bj)] (bi <= bj, diagonal blocks FULL) holds
+// B[4q + r][col] in lane (q, col).  Row products B v_bj go to y_bi (summed
+// over the 16 lanes of a q-group), column products B^T v_bi of the
+// off-diagonal blocks to y_bj (summed over the 4 q-groups), both through LDS
+// in a fixed order.  v in sc.pv (virtual order).  Returns y at virtual
+// o = lane + 64 h in yo[h] (without the bias column) -- 0 for padding.
+template <int NB>
+__device__ __forceinline__ void acc_matvec(const floatx4 (&acc)[NB * (NB + 1) / 2],
+                                           StartScratch<NB>& sc, int k,
+                                           float (&yo)[(16 * NB + 63) / 64]) {
+  constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
+  const int lane = threadIdx.x & 63, q = lane >> 4, col = lane & 15;
+  float R[NB][4], Cp[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    Cp[b] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) R[b][r] = 0.f;
+  }
+  int t = 0;
+#pragma unroll
+  for (int bi = 0; bi < NB; ++bi) {
+    const float4 vq = *reinterpret_cast<const float4*>(&sc.pv[16 * bi + 4 * q]);
+#pragma unroll
+    for (int bj = bi; bj < NB; ++bj) {
+      const float vj = sc.pv[16 * bj + col];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) R[bi][r] = fmaf(acc[t][r], vj, R[bi][r]);
+      if (bi != bj) {
+        float c = Cp[bj];
+        c = fmaf(acc[t][0], vq.x, c);
+        c = fmaf(acc[t][1], vq.y, c);
+        c = fmaf(acc[t][2], vq.z, c);
+        c = fmaf(acc[t][3], vq.w, c);
+        Cp[bj] = c;
+      }
+      ++t;
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sc.partR[4 * b + r][lane] = R[b][r];
+    sc.partC[b][lane] = Cp[b];
+  }
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int h = 0; h < NV; ++h) {
+    const int o = lane + 64 * h;
+    yo[h] = 0.f;
+    if (o >= NP || nat_of(o, NB) >= k) continue;
+    const int b = o >> 4, i = o & 15, qq = i >> 2, rr = i & 3;
+    const float4* pr = reinterpret_cast<const float4*>(&sc.partR[4 * b + rr][16 * qq]);
+    const float4 a0 = pr[0], a1 = pr[1], a2 = pr[2], a3 = pr[3];
+    const float s0 = ((a0.x + a0.y) + (a0.z + a0.w)) + ((a1.x + a1.y) + (a1.z + a1.w));
+    const float s1 = ((a2.x + a2.y) + (a2.z + a2.w)) + ((a3.x + a3.y) + (a3.z + a3.w));
+    const float c = (sc.partC[b][i] + sc.partC[b][16 + i]) +
+                    (sc.partC[b][32 + i] + sc.partC[b][48 + i]);
+    yo[h] = (s0 + s1) + c;
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Fused CG start of one unsplit entity from the Gram wave's registers
+// (cg_least_squares, matrix.cpp:464-476 and iteration 0's matvec / dot,
+// :493-497, in block form): r0 = G x - c, p0 = -r0, q0 = G p0, written to
+// the CG vectors; adds r0.r0 to drr and p0.q0 to dpq (fp64, lane partials
+// summed across the wave).  cacc / sacc: c and the row sums at virtual
+// (b, col) in every lane (already reduced over q); wt / gn: user-side
+// sum of ratings and count; xv / xb: x at virtual (b, col) and its bias.
+template <int NB, bool USER>
+__device__ __forceinline__ void start_from_acc(const floatx4 (&acc)[NB * (NB + 1) / 2],
+                                               const float (&cacc)[NB], const float (&sacc)[NB],
+                                               float wt, float gn, const float (&xv)[NB],
+                                               float xb, int64_t e, int k, int ldk,
+                                               const CgStart& cs, StartScratch<NB>& sc,
+                                               double& drr, double& dpq) {
+  constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
+  const int lane = threadIdx.x & 63, q = lane >> 4, col = lane & 15;
+  if (q == 0) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const bool live = NB * col + b < k;   // natural column of virtual (b, col)
+      sc.pv[16 * b + col] = xv[b];
+      sc.sC[16 * b + col] = live ? cacc[b] : 0.f;
+      if (USER) sc.sGs[16 * b + col] = live ? sacc[b] : 0.f;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  float yo[NV];
+  acc_matvec<NB>(acc, sc, k, yo);
+  // r0 = G x - c (+ bias column), p0 = -r0; user bias row: Gs.x + Gn xb - Cb
+  double d = 0.0;
+  float ybp = 0.f, pn[NV];
+#pragma unroll
+  for (int h = 0; h < NV; ++h) {
+    const int o = lane + 64 * h;
+    pn[h] = 0.f;
+    if (o < NP) {
+      const int n = nat_of(o, NB);
+      if (n < k) {
+        float y = yo[h];
+        if (USER) {
+          const float gs = sc.sGs[o];
+          y = fmaf(gs, xb, y);
+          ybp = fmaf(gs, sc.pv[o], ybp);
+        }
+        const float rv = y - sc.sC[o];
+        cs.r[e * ldk + n] = rv;
+        cs.p[e * ldk + n] = -rv;
+        d += (double)rv * rv;
+        pn[h] = -rv;
+      }
+    }
+  }
+  float pb = 0.f;
+  if (USER) {
+    const float rbv = fmaf(gn, xb, wave_sum_f32(ybp)) - wt;
+    pb = -rbv;
+    if (lane == 0) {
+      cs.rb[e] = rbv;
+      cs.pb[e] = pb;
+      d += (double)rbv * rbv;
+    }
+  }
+  drr += wave_sum_f64(d);
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int h = 0; h < NV; ++h) {
+    const int o = lane + 64 * h;
+    if (o < NP) sc.pv[o] = pn[h];
+  }
+  __builtin_amdgcn_wave_barrier();
+  // q0 = G p0 (+ bias column), p0.q0
+  acc_matvec<NB>(acc, sc, k, yo);
+  d = 0.0;
+  ybp = 0.f;
+#pragma unroll
+  for (int h = 0; h < NV; ++h) {
+    const int o = lane + 64 * h;
+    if (o < NP) {
+      const int n = nat_of(o, NB);
+      if (n < k) {
+        float y = yo[h];
+        if (USER) {
+          const float gs = sc.sGs[o];
+          y = fmaf(gs, pb, y);
+          ybp = fmaf(gs, pn[h], ybp);
+        }
+        cs.q[e * ldk + n] = y;
+        d += (double)y * pn[h];
+      }
+    }
+  }
+  if (USER) {
+    const float qb = fmaf(gn, pb, wave_sum_f32(ybp));
+    if (lane == 0) {
+      cs.qb[e] = qb;
+      d += (double)qb * pb;
+    }
+  }
+  dpq += wave_sum_f64(d);
+}
+
 // ---------------------------------------------------------------------------
 // K1: gather-Gram.  One wave per WorkItem (an entity, or a chunk of a heavy
 // entity).  Rows a_r are gathered from the opposite factor table (row stride
@@ -66,7 +507,6 @@ __device__ __forceinline__ double block_sum_f64(double v, double* sh) {
 // Rows of UNR steps are gathered before their MFMAs (UNR*NB loads in flight
 // per wave).
 // ---------------------------------------------------------------------------
-typedef float floatx4 __attribute__((ext_vector_type(4)));
 constexpr int GRAM_WAVES = 4;
 
 // Per-lane copy of one 64-rating chunk: opposite id, rating and (item side)
@@ -188,18 +628,16 @@ __device__ __forceinline__ void mfma_group(floatx4 (&acc)[NB * (NB + 1) / 2],
   }
 }
 
-template <int NB, int G, bool USER, bool NTS>
-__global__ __launch_bounds__(256) void gram_kernel(
-    const WorkItem* __restrict__ work, int64_t n_work,
+template <int NB, int G, bool USER, bool NTS, bool FUSE>
+__device__ __forceinline__ void gram_wave(
+    int64_t wi, const WorkItem* __restrict__ work,
     const int32_t* __restrict__ idx, const float* __restrict__ val,
     const float* __restrict__ F, const float* __restrict__ bias, int k, int ldk, int zrow,
-    GramDst direct, GramDst slab) {
+    const GramDst& direct, const GramDst& slab, const CgStart& cs, StartScratch<NB>* ssc,
+    double& drr, double& dpq) {
   constexpr int T = NB * (NB + 1) / 2;
   constexpr int GPC = 16 / G;              // groups per 64-rating chunk
   const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t wi = (int64_t)blockIdx.x * GRAM_WAVES + wid;
-  if (wi >= n_work) return;  // waves are independent: no block barriers below
   // work-item fields in SGPRs: all control flow below is scalar
   const int64_t wbeg = work[wi].begin;
   const int wlen = work[wi].len;
@@ -211,6 +649,16 @@ __global__ __launch_bounds__(256) void gram_kernel(
   const int ngroups = (nst + G - 1) / G;
   const uint32_t row_bytes = (uint32_t)ldk * 4u;
   const char* Fc = reinterpret_cast<const char*>(F) + 4 * NB * col;
+
+  // fused CG start: this lane's x entries (virtual (b, col) = natural
+  // NB*col + b, contiguous) are fetched now and used after the loop
+  float xv[NB];
+  float xbv = 0.f;
+  if constexpr (FUSE) {
+    const int64_t xe = (wslab < 0) ? (int64_t)went : 0;
+    load_row_seg<NB>(xv, cs.x + xe * ldk + NB * col);
+    if (USER) xbv = cs.xb[xe];
+  }
 
   floatx4 acc[T];
 #pragma unroll
@@ -313,26 +761,80 @@ __global__ __launch_bounds__(256) void gram_kernel(
       ++t;
     }
   }
+  if constexpr (FUSE) {
+    if (!to_slab) {
+      const float wt = USER ? (__shfl(wsum, 0, 64) + __shfl(wsum, 16, 64)) +
+                                  (__shfl(wsum, 32, 64) + __shfl(wsum, 48, 64))
+                            : 0.f;
+      start_from_acc<NB, USER>(acc, cacc, sacc, wt, (float)wlen, xv, xbv, went, k, ldk, cs,
+                               *ssc, drr, dpq);
+    }
+  }
+}
+
+// Waves are independent: one work item each, no block barriers -- except in
+// the FUSE form, whose waves then start the CG solve on their entity
+// (cg_start_entity; split entities are started after slab_reduce) and meet
+// once at the end to store the block's (r.r, p.Gp) pair.
+#ifndef MR_GRAM_WPE
+#define MR_GRAM_WPE 1
+#endif
+template <int NB, int G, bool USER, bool NTS, bool FUSE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR_GRAM_WPE))) void gram_kernel(
+    const WorkItem* __restrict__ work, int64_t n_work,
+    const int32_t* __restrict__ idx, const float* __restrict__ val,
+    const float* __restrict__ F, const float* __restrict__ bias, int k, int ldk, int zrow,
+    GramDst direct, GramDst slab, CgStart cs) {
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t wi = (int64_t)blockIdx.x * GRAM_WAVES + wid;
+  double drr = 0.0, dpq = 0.0;
+  if constexpr (!FUSE) {
+    if (wi >= n_work) return;
+    gram_wave<NB, G, USER, NTS, false>(wi, work, idx, val, F, bias, k, ldk, zrow, direct, slab,
+                                       cs, nullptr, drr, dpq);
+  } else {
+    __shared__ StartScratch<NB> scr[GRAM_WAVES];
+    if (wi < n_work)
+      gram_wave<NB, G, USER, NTS, true>(wi, work, idx, val, F, bias, k, ldk, zrow, direct, slab,
+                                        cs, &scr[wid], drr, dpq);
+    store_start_pair(drr, dpq, cs.parts);
+  }
+}
+
+// Split entities: the CG start after slab_reduce (one wave per entity).
+template <int NB, bool USER>
+__global__ __launch_bounds__(256) void cg_start_split_kernel(const SplitItem* __restrict__ split,
+                                                             int64_t n_split, int k, int ldk,
+                                                             GramDst direct, CgStart cs,
+                                                             double* __restrict__ parts) {
+  __shared__ MvScratch<NB> scr[4];
+  const int wid = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 4 + wid;
+  double drr = 0.0, dpq = 0.0;
+  if (i < n_split) cg_start_entity<NB, USER>(split[i].entity, k, ldk, direct, cs, scr[wid], drr, dpq);
+  store_start_pair(drr, dpq, parts);
 }
 
 template <int NB, int G>
 static int launch_gram_g(hipStream_t s, bool user_side, int k, const WorkItem* work,
                          int64_t n_work, const int32_t* idx, const float* val,
                          const float* F, const float* bias, int zrow, GramDst direct,
-                         GramDst slab) {
+                         GramDst slab, const CgStart* start) {
   const int64_t grid = (n_work + GRAM_WAVES - 1) / GRAM_WAVES;
-  static int nts = -1;
-  if (nts < 0) {
-    const char* e = getenv("MR_GRAM_NT_STORE");
-    nts = (e && atoi(e) == 1) ? 1 : 0;
+  const CgStart cs = start ? *start : CgStart{};
+  // MR_GRAM_LDS=bytes: extra dynamic LDS per block (caps blocks per CU; tuning)
+  static int lds = -1;
+  if (lds < 0) {
+    const char* e = getenv("MR_GRAM_LDS");
+    lds = e ? atoi(e) : 0;
   }
-#define MR_GRAM_LAUNCH(U, N)                                                  \
-  MR_LAUNCH((gram_kernel<NB, G, U, N>), dim3((unsigned)grid), dim3(256), 0, s, \
-            work, n_work, idx, val, F, bias, k, ldk_of(k), zrow, direct, slab)
+#define MR_GRAM_LAUNCH(U, FU)                                                     \
+  MR_LAUNCH((gram_kernel<NB, G, U, false, FU>), dim3((unsigned)grid), dim3(256), lds, s, \
+            work, n_work, idx, val, F, bias, k, ldk_of(k), zrow, direct, slab, cs)
   if (user_side) {
-    if (nts) MR_GRAM_LAUNCH(true, true); else MR_GRAM_LAUNCH(true, false);
+    if (start) MR_GRAM_LAUNCH(true, true); else MR_GRAM_LAUNCH(true, false);
   } else {
-    if (nts) MR_GRAM_LAUNCH(false, true); else MR_GRAM_LAUNCH(false, false);
+    if (start) MR_GRAM_LAUNCH(false, true); else MR_GRAM_LAUNCH(false, false);
   }
 #undef MR_GRAM_LAUNCH
   MR_HIP(hipGetLastError());
@@ -356,27 +858,51 @@ template <int NB>
 static int launch_gram_nb(hipStream_t s, bool user_side, int k, const WorkItem* work,
                           int64_t n_work, const int32_t* idx, const float* val,
                           const float* F, const float* bias, int zrow, GramDst direct,
-                          GramDst slab) {
+                          GramDst slab, const CgStart* start) {
   if (n_work <= 0) return 0;
   switch (gram_group_size(NB)) {
-    case 2: return launch_gram_g<NB, 2>(s, user_side, k, work, n_work, idx, val, F, bias, zrow, direct, slab);
-    case 4: return launch_gram_g<NB, 4>(s, user_side, k, work, n_work, idx, val, F, bias, zrow, direct, slab);
-    default: return launch_gram_g<NB, 8>(s, user_side, k, work, n_work, idx, val, F, bias, zrow, direct, slab);
+    case 2: return launch_gram_g<NB, 2>(s, user_side, k, work, n_work, idx, val, F, bias, zrow, direct, slab, start);
+    case 4: return launch_gram_g<NB, 4>(s, user_side, k, work, n_work, idx, val, F, bias, zrow, direct, slab, start);
+    default: return launch_gram_g<NB, 8>(s, user_side, k, work, n_work, idx, val, F, bias, zrow, direct, slab, start);
   }
 }
 
 int launch_gram(hipStream_t s, bool user_side, int k, const WorkItem* work,
                 int64_t n_work, const int32_t* idx, const float* val,
                 const float* F, const float* bias, int zrow, GramDst direct,
-                GramDst slab) {
+                GramDst slab, const CgStart* start) {
 #define MR_GRAM_CASE(NB) \
-  case NB: return launch_gram_nb<NB>(s, user_side, k, work, n_work, idx, val, F, bias, zrow, direct, slab);
+  case NB: return launch_gram_nb<NB>(s, user_side, k, work, n_work, idx, val, F, bias, zrow, direct, slab, start);
   switch (nb16_of(k)) {
     MR_GRAM_CASE(1) MR_GRAM_CASE(2) MR_GRAM_CASE(3) MR_GRAM_CASE(4)
     MR_GRAM_CASE(5) MR_GRAM_CASE(6) MR_GRAM_CASE(7) MR_GRAM_CASE(8)
     default: set_error("k > 128 not supported by the Gram kernel"); return -1;
   }
 #undef MR_GRAM_CASE
+}
+
+int launch_cg_start_split(hipStream_t s, bool user_side, int k, const SplitItem* split,
+                          int64_t n_split, GramDst direct, const CgStart& cs, double* parts) {
+  if (n_split <= 0) return 0;
+  const unsigned grid = (unsigned)((n_split + 3) / 4);
+  const int ldk = ldk_of(k);
+#define MR_SS_CASE(NB)                                                                      \
+  case NB:                                                                                  \
+    if (user_side)                                                                          \
+      MR_LAUNCH((cg_start_split_kernel<NB, true>), dim3(grid), dim3(256), 0, s, split, n_split, \
+                k, ldk, direct, cs, parts);                                                 \
+    else                                                                                    \
+      MR_LAUNCH((cg_start_split_kernel<NB, false>), dim3(grid), dim3(256), 0, s, split,     \
+                n_split, k, ldk, direct, cs, parts);                                        \
+    break;
+  switch (nb16_of(k)) {
+    MR_SS_CASE(1) MR_SS_CASE(2) MR_SS_CASE(3) MR_SS_CASE(4)
+    MR_SS_CASE(5) MR_SS_CASE(6) MR_SS_CASE(7) MR_SS_CASE(8)
+    default: set_error("k > 128 not supported"); return -1;
+  }
+#undef MR_SS_CASE
+  MR_HIP(hipGetLastError());
+  return 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -542,7 +1068,6 @@ __device__ void last_block_finalize(CgState* st, int phase, double* partials, Cg
   }
 }
 
-constexpr int MV_WAVES = 4;
 
 template <int NB, bool USER, bool NT>
 __global__ __launch_bounds__(256) void cg_matvec_kernel(
@@ -555,22 +1080,17 @@ __global__ __launch_bounds__(256) void cg_matvec_kernel(
   if (st->done) return;
   constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2, NTILE = NO + NF + (NB & 1);
   constexpr int64_t GS = (int64_t)NTILE * 256 + NF * 16;   // == gsize_of(k)
-  constexpr int NP = 16 * NB;
-  constexpr int CST = 68;   // float4 stride of a column-partial row (+16 floats: no bank clash)
-  __shared__ float pv[MV_WAVES][NP];
-  __shared__ float redR[MV_WAVES][NB][64];
-  __shared__ float4 redC[MV_WAVES][NB][CST];
-  __shared__ float dd[MV_WAVES][NF > 0 ? 16 * NF : 1];
+  constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
+  __shared__ MvScratch<NB> scr[MV_WAVES];
   __shared__ double sh[MV_WAVES];
   const float beta = (float)st->beta;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int rr = lane >> 2, c4 = (lane & 3) * 4;
+  MvScratch<NB>& sc = scr[wid];
   double dsum = 0.0;
   for (int64_t e = (int64_t)blockIdx.x * MV_WAVES + wid; e < E;
        e += (int64_t)gridDim.x * MV_WAVES) {
     // issue order matters for the in-order vmcnt: vector loads first, then
     // every G block of this entity, so staging p waits only for the former
-    constexpr int NV = (NP + 63) / 64;
     float* ve = v + e * ldk;
     float vi[NV], ri[NV];
 #pragma unroll
@@ -607,116 +1127,33 @@ __global__ __launch_bounds__(256) void cg_matvec_kernel(
           x = fmaf(beta, x, -ri[h]);
           ve[i] = x;
         }
-        pv[wid][virt_of(i, NB)] = x;
+        sc.pv[virt_of(i, NB)] = x;
       }
     }
     if (USER && update_p) {
       vbias = fmaf(beta, vbias, -rbias);
       if (lane == 0) vb[e] = vbias;
     }
-    if (NF > 0 && lane < 16 * NF) dd[wid][lane] = d2;
+    if (NF > 0 && lane < 16 * NF) sc.dd[lane] = d2;
     __builtin_amdgcn_wave_barrier();
-    float accR[NB];
-    float4 accC[NB];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      accR[b] = 0.f;
-      accC[b] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    // strictly-upper tiles: row product into y_bi, column product into y_bj
-    int t = 0;
-#pragma unroll
-    for (int bi = 0; bi < NB; ++bi) {
-      const float pi = pv[wid][16 * bi + rr];
-#pragma unroll
-      for (int bj = bi + 1; bj < NB; ++bj) {
-        const float4 gg = g[t];
-        const float4 pj = *reinterpret_cast<const float4*>(&pv[wid][16 * bj + c4]);
-        float s0 = accR[bi];
-        s0 = fmaf(gg.x, pj.x, s0);
-        s0 = fmaf(gg.y, pj.y, s0);
-        s0 = fmaf(gg.z, pj.z, s0);
-        s0 = fmaf(gg.w, pj.w, s0);
-        accR[bi] = s0;
-        accC[bj].x = fmaf(gg.x, pi, accC[bj].x);
-        accC[bj].y = fmaf(gg.y, pi, accC[bj].y);
-        accC[bj].z = fmaf(gg.z, pi, accC[bj].z);
-        accC[bj].w = fmaf(gg.w, pi, accC[bj].w);
-        ++t;
-      }
-    }
-    // folded diagonal tiles: c >= r belongs to D_2m (row; column also for
-    // c > r), c < r to D_2m+1 (row and column)
-#pragma unroll
-    for (int m = 0; m < NF; ++m) {
-      const int b0 = 2 * m, b1 = 2 * m + 1;
-      const float4 gg = g[NO + m];
-      const float ge[4] = {gg.x, gg.y, gg.z, gg.w};
-      const float4 p0 = *reinterpret_cast<const float4*>(&pv[wid][16 * b0 + c4]);
-      const float4 p1 = *reinterpret_cast<const float4*>(&pv[wid][16 * b1 + c4]);
-      const float p0c[4] = {p0.x, p0.y, p0.z, p0.w};
-      const float p1c[4] = {p1.x, p1.y, p1.z, p1.w};
-      const float pr0 = pv[wid][16 * b0 + rr], pr1 = pv[wid][16 * b1 + rr];
-      float c0[4], c1[4];
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        const int c = c4 + x;
-        const float gu = (c >= rr) ? ge[x] : 0.f;
-        const float gc = (c > rr) ? ge[x] : 0.f;
-        const float gl = (c < rr) ? ge[x] : 0.f;
-        accR[b0] = fmaf(gu, p0c[x], accR[b0]);
-        accR[b1] = fmaf(gl, p1c[x], accR[b1]);
-        c0[x] = gc * pr0;
-        c1[x] = gl * pr1;
-      }
-      accC[b0].x += c0[0]; accC[b0].y += c0[1]; accC[b0].z += c0[2]; accC[b0].w += c0[3];
-      accC[b1].x += c1[0]; accC[b1].y += c1[1]; accC[b1].z += c1[2]; accC[b1].w += c1[3];
-    }
-    if constexpr ((NB & 1) != 0) {   // last diagonal block stored full: row product
-      const float4 gg = g[NO + NF];
-      const float4 pj = *reinterpret_cast<const float4*>(&pv[wid][16 * (NB - 1) + c4]);
-      float s0 = accR[NB - 1];
-      s0 = fmaf(gg.x, pj.x, s0);
-      s0 = fmaf(gg.y, pj.y, s0);
-      s0 = fmaf(gg.z, pj.z, s0);
-      s0 = fmaf(gg.w, pj.w, s0);
-      accR[NB - 1] = s0;
-    }
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      redR[wid][b][lane] = accR[b];
-      redC[wid][b][lane] = accC[b];
-    }
-    __builtin_amdgcn_wave_barrier();
+    float yo[NV], ybv = 0.f;
+    tile_matvec<NB, USER>(g, sc, vbias, USER ? Gs + e * ldk : nullptr, USER ? Gn[e] : 0.f, k,
+                          yo, ybv);
     double d = 0.0;
-    float ybp = 0.f;
-    for (int o = lane; o < NP; o += 64) {   // o: virtual index
-      const int n = nat_of(o, NB);
-      if (n >= k) continue;
-      const int b = o >> 4, ii = o & 15;
-      const float* R = &redR[wid][b][4 * ii];
-      float yo = (R[0] + R[1]) + (R[2] + R[3]);
-      const float* C = reinterpret_cast<const float*>(&redC[wid][b][0]) + ii;
-      float sc = 0.f;
 #pragma unroll
-      for (int qq = 0; qq < 16; ++qq) sc += C[16 * qq];
-      yo += sc;
-      if (NF > 0 && (b & 1) && b < 2 * NF) yo = fmaf(dd[wid][(b >> 1) * 16 + ii], pv[wid][o], yo);
-      if (USER) {
-        const float gs = Gs[e * ldk + n];
-        yo = fmaf(gs, vbias, yo);
-        ybp = fmaf(gs, pv[wid][o], ybp);
+    for (int h = 0; h < NV; ++h) {
+      const int o = lane + 64 * h;
+      if (o < NP) {
+        const int n = nat_of(o, NB);
+        if (n < k) {
+          y[e * ldk + n] = yo[h];
+          d += (double)yo[h] * sc.pv[o];
+        }
       }
-      y[e * ldk + n] = yo;
-      d += (double)yo * pv[wid][o];
     }
-    if (USER) {
-      const float yb_s = wave_sum_f32(ybp);
-      const float ybv = fmaf(Gn[e], vbias, yb_s);
-      if (lane == 0) {
-        yb[e] = ybv;
-        d += (double)ybv * vbias;
-      }
+    if (USER && lane == 0) {
+      yb[e] = ybv;
+      d += (double)ybv * vbias;
     }
     dsum += wave_sum_f64(d);
     __builtin_amdgcn_wave_barrier();
@@ -867,25 +1304,81 @@ int launch_cg_update(hipStream_t s, const CgState* st, int mode, int64_t n,
 // all-reduce that slot next); CTL_FINALIZE applies the rules from comm[0].
 // ---------------------------------------------------------------------------
 
-__global__ __launch_bounds__(256) void cg_control_kernel(
+constexpr int CTL_THREADS = 1024;
+__global__ __launch_bounds__(CTL_THREADS) void cg_control_kernel(
     CgState* __restrict__ st, int phase, int ctl,
-    const double* __restrict__ partials, int n_part, CgMirror* mirror, int seq) {
-  if (phase != CG_INIT && st->done) return;
-  __shared__ double sh[4];
+    const double* __restrict__ partials, int n_part, CgMirror* mirror, int seq,
+    double min_dec, int max_it, int sharded) {
+  if (phase != CG_INIT && phase != CG_START && st->done) return;
+  __shared__ double sh[CTL_THREADS / 64];
   if (ctl & CTL_REDUCE) {
-    double acc = 0.0;
-    for (int i = threadIdx.x; i < n_part; i += blockDim.x) acc += partials[i];
-    const double tot = block_sum_f64<256>(acc, sh);
-    if (threadIdx.x == 0) st->comm[0] = tot;
+    if (phase == CG_START) {
+      // (r.r, p.Gp) pairs (one per Gram block: ~E/4 of them, written by
+      // every XCD): thread t sums pairs t, t + T, t + 2T, ... in order, 8
+      // coalesced loads in flight, then the fixed-order block tree.
+      const double2* pp = reinterpret_cast<const double2*>(partials);
+      double a = 0.0, b = 0.0;
+      for (int base = 0; base < n_part; base += 8 * CTL_THREADS) {
+        double2 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int i = base + j * CTL_THREADS + threadIdx.x;
+          v[j] = (i < n_part) ? pp[i] : make_double2(0.0, 0.0);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          a += v[j].x;
+          b += v[j].y;
+        }
+      }
+      const double ta = block_sum_f64<CTL_THREADS>(a, sh);
+      __syncthreads();
+      const double tb = block_sum_f64<CTL_THREADS>(b, sh);
+      if (threadIdx.x == 0) {
+        st->comm[0] = ta;
+        st->comm[1] = tb;
+      }
+    } else {
+      double acc = 0.0;
+      for (int i = threadIdx.x; i < n_part; i += blockDim.x) acc += partials[i];
+      const double tot = block_sum_f64<CTL_THREADS>(acc, sh);
+      if (threadIdx.x == 0) st->comm[0] = tot;
+    }
   }
   if (threadIdx.x != 0 || !(ctl & CTL_FINALIZE)) return;
+  if (phase == CG_START) {
+    // fresh state (cg_least_squares entry), then the INIT rule on r0.r0 and,
+    // unless that ended the solve, alpha of iteration 0 from p0.G p0
+    const double rr = st->comm[0], pq = st->comm[1];
+    st->min_dec = min_dec;
+    st->max_it = max_it;
+    st->sharded = sharded;
+    st->arrive = 0;
+    st->n_matvec = 0;
+    st->alpha = 0.0;
+    st->beta = 0.0;
+    st->rr = rr;
+    st->final_rr = rr;
+    st->it = 0;
+    st->fails = 0;
+    st->ret = 0;
+    st->done = (max_it <= 0 || rr < 1e-6) ? 1 : 0;
+    if (!st->done) {
+      st->alpha = rr / pq;
+      st->comm[0] = pq;      // sharded updates derive alpha as rr / comm[0]
+      st->n_matvec = 1;      // the fused iteration-0 matvec
+    }
+    publish(st, mirror, seq);
+    return;
+  }
   cg_finalize(st, phase, st->comm[0], mirror, seq);
 }
 
 int launch_cg_control(hipStream_t s, CgState* st, int phase, int ctl,
-                      const double* partials, int n_part, CgMirror* mirror, int seq) {
-  MR_LAUNCH(cg_control_kernel, dim3(1), dim3(256), 0, s, st, phase, ctl, partials, n_part,
-                                                  mirror, seq);
+                      const double* partials, int n_part, CgMirror* mirror, int seq,
+                      double min_dec, int max_it, int sharded) {
+  MR_LAUNCH(cg_control_kernel, dim3(1), dim3(CTL_THREADS), 0, s, st, phase, ctl, partials, n_part,
+                                                  mirror, seq, min_dec, max_it, sharded);
   MR_HIP(hipGetLastError());
   return 0;
 }

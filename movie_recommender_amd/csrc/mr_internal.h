@@ -129,6 +129,16 @@ struct GramDst {
   int64_t sG, sV, sS;
 };
 
+// Fused CG start (Gram epilogue): the iterate and the CG vectors of one side,
+// and the (r.r, p.Gp) pair slots, one pair per Gram block then one per
+// split-start block.
+struct CgStart {
+  const float* x;    // this side's iterate (local rows), ldk stride
+  const float* xb;   // user side: bias column of the iterate
+  float *r, *rb, *p, *pb, *q, *qb;
+  double* parts;
+};
+
 // CG scalar state, device resident (matrix.cpp:456-529 scalars).
 struct CgState {
   double rr;        // r.r of the current iterate
@@ -161,16 +171,25 @@ struct CgMirror {
   double final_rr;
 };
 
-enum CgPhase { CG_INIT = 0, CG_ALPHA = 1, CG_BETA = 2 };
+// CG_START: INIT then ALPHA on a fused start's (r.r, p.Gp) pair sums; the
+// control kernel also (re)initialises the state from its arguments.
+enum CgPhase { CG_INIT = 0, CG_ALPHA = 1, CG_BETA = 2, CG_START = 3 };
 enum CgCtl { CTL_REDUCE = 1, CTL_FINALIZE = 2, CTL_BOTH = 3 };
 enum CgUpd { UPD_INIT = 0, UPD_STEP = 1 };
 
 // Kernel launchers (kernels.hip) ---------------------------------------------
 // F has zrow+1 rows; row zrow (and bias[zrow]) is all zero.
+// start != nullptr: every wave also starts the CG solve on its (unsplit)
+// entity -- r0 = Gx - c, p0 = -r0, q0 = G p0 -- and each block stores its
+// (r.r, p.Gp) pair to start->parts[2 * block]; split entities follow with
+// launch_cg_start_split after slab_reduce (pairs after the Gram blocks').
 int launch_gram(hipStream_t s, bool user_side, int k, const WorkItem* work,
                 int64_t n_work, const int32_t* idx, const float* val,
                 const float* F, const float* bias, int zrow, GramDst direct,
-                GramDst slab);
+                GramDst slab, const CgStart* start = nullptr);
+inline int64_t gram_blocks(int64_t n_work) { return (n_work + 3) / 4; }
+int launch_cg_start_split(hipStream_t s, bool user_side, int k, const SplitItem* split,
+                          int64_t n_split, GramDst direct, const CgStart& cs, double* parts);
 // bf16x3 normal equations (gram3.hip): Fs = launch_split_table(F) once per
 // half-step, rows x 3 parts x ldk bf16 in virtual column order.
 bool gram3_supported(int k);
@@ -196,9 +215,11 @@ int launch_cg_update(hipStream_t s, const CgState* st, int mode, int64_t n,
                      const float* qb, const float* cb, double* partials,
                      int n_part, CgState* fst = nullptr, CgMirror* mirror = nullptr,
                      int seq = 0);
+// phase CG_START: partials are n_part (r.r, p.Gp) pairs; min_dec / max_it /
+// sharded initialise the state.
 int launch_cg_control(hipStream_t s, CgState* st, int phase, int ctl,
                       const double* partials, int n_part, CgMirror* mirror = nullptr,
-                      int seq = 0);
+                      int seq = 0, double min_dec = 0.0, int max_it = 0, int sharded = 0);
 int launch_solve(hipStream_t s, bool user_side, int64_t E, int k, double ridge,
                  const float* G, const float* Gs, const float* Gn,
                  const float* C, const float* Cb, float* x, float* xb,
