@@ -62,9 +62,12 @@ def algorithmic_cost(cls, k, n_users, n_items, n_ratings, ldk):
     nb/2 tiles (+1 full tile for odd nb) and a 16-float diagonal side array
     per fold, nb = ceil(k/16) -- 2080 floats at k = 64 (k(k+1)/2 = 2080).  The
     CG matvec's bytes are that storage plus the CG vectors it streams.  Gram
-    flops are the full K x K outer products of SURVEY.md 8(d) F(k) (the kernel
-    computes only the upper blocks, so its MFMA work is nb(nb+1)/2*512 flop
-    per rating)."""
+    flops count each of the K(K+1)/2 distinct entries of the symmetric
+    per-rating outer product once (2 flop each) plus the rhs (2K) -- the
+    minimum work; SURVEY.md 8(d)'s F(k) counts the full K x K product, which
+    would put a symmetric kernel above the MFMA peak.  The kernel's executed
+    MFMA work is nb(nb+1)/2 * 512 flop per rating (diagonal blocks full).
+    With the fused CG start (default) the Gram launch also writes r, p, q."""
     K = k + 1
     nb = (k + 15) // 16
     gsz = (nb * (nb - 1) // 2 + nb // 2 + nb % 2) * 256 + (nb // 2) * 16
@@ -76,13 +79,18 @@ def algorithmic_cost(cls, k, n_users, n_items, n_ratings, ldk):
     if cls == "matvec_items":
         E = n_items
         return E * gsz * 4 + E * ldk * 4 * 4, E * 2.0 * k * k
+    fused = os.environ.get("MR_FUSE_START", "1") != "0"
     if cls == "gram_users":
         # per rating: (idx, value) 8 B + gathered item row k*4 B; output blocks
         b = n_ratings * (8 + 4 * k) + n_users * (gsz + 2 * ldk + 2) * 4
-        return b, n_ratings * (2.0 * K * K + 2.0 * K)
+        if fused:   # x read, r / p / q written
+            b += n_users * (ldk + 1) * 4 * 4
+        return b, n_ratings * (1.0 * K * (K + 1) + 2.0 * K)
     if cls == "gram_items":
         b = n_ratings * (8 + 4 * (k + 1)) + n_items * (gsz + ldk) * 4
-        return b, n_ratings * (2.0 * k * k + 2.0 * k)
+        if fused:
+            b += n_items * ldk * 4 * 4
+        return b, n_ratings * (1.0 * k * (k + 1) + 2.0 * k)
     if cls == "cg_update":
         E = (n_users * (ldk + 1) + n_items * ldk) / 2.0   # average side
         return E * 6 * 4, E * 4.0
@@ -128,7 +136,7 @@ def cpu_baseline(rs, k, threads, frac, seed=0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--k", type=int, default=64)
     ap.add_argument("--shape", default="ml-full")

@@ -17,6 +17,13 @@
 
 #include "mr_internal.h"
 
+// Tuning switch (build-time; tools/build_variant.sh): row buffers of the
+// Gram main loop (groups in flight + 1).  Measured on MI355X (ML-full shape,
+// k = 64, tools/ab_gram.sh): 4 buffers of G = 2 steps is best.
+#ifndef MR_GRAM_NBUF
+#define MR_GRAM_NBUF 4
+#endif
+
 namespace mr {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -509,12 +516,11 @@ __device__ __forceinline__ void start_from_acc(const floatx4 (&acc)[NB * (NB + 1
 // ---------------------------------------------------------------------------
 constexpr int GRAM_WAVES = 4;
 
-// Per-lane copy of one 64-rating chunk: opposite id, rating and (item side)
-// the opposite bias.  Slots past the end of the work item point at the
-// table's all-zero row `zrow` with rating 0, so gathers and MFMAs need no
-// masks.  The weight w = r - bias is formed only when the chunk becomes
-// current (one chunk after its loads were issued), so no load is waited on
-// early.
+// Per-lane raw loads of one 64-rating chunk: opposite id, rating and (item
+// side) the opposite bias.  Lanes past the end of the work item load from a
+// safe in-range address; finish_raw masks them (id -> the all-zero row
+// `zrow`, weight 0) only when the chunk becomes current, so no select waits
+// on a load that was just issued.
 struct ChunkRaw {
   int idx;
   float r;
@@ -525,34 +531,37 @@ struct ChunkRegs {
   float w;
 };
 
-// Stage 1 of a chunk: ids and ratings (independent loads).
-__device__ __forceinline__ ChunkRaw load_chunk(const int32_t* __restrict__ idx,
-                                               const float* __restrict__ val,
-                                               int64_t begin, int64_t end, int c,
-                                               int lane, int zrow) {
+__device__ __forceinline__ ChunkRaw load_chunk_raw(const int32_t* __restrict__ idx,
+                                                   const float* __restrict__ val,
+                                                   int64_t begin, int64_t end, int64_t safe,
+                                                   int c, int lane) {
   const int64_t jj = begin + 64 * (int64_t)c + lane;
-  const bool ok = jj < end;
-  const int64_t js = ok ? jj : begin;           // always a valid address
+  const int64_t js = jj < end ? jj : safe;
   ChunkRaw r;
-  const int i0 = idx[js];
-  const float v0 = val[js];
-  r.idx = ok ? i0 : zrow;
-  r.r = ok ? v0 : 0.f;
+  r.idx = idx[js];
+  r.r = val[js];
   r.b = 0.f;
   return r;
 }
 
-// Stage 2 (item side): the opposite bias, gathered through the ids loaded
-// one rotation earlier (bias[zrow] == 0).
+// Item side: the opposite bias, gathered through ids loaded one chunk earlier
+// (masked lanes read bias[zrow] == 0).
 template <bool USER>
-__device__ __forceinline__ void load_bias(ChunkRaw& c, const float* __restrict__ bias) {
-  if (!USER) c.b = bias[c.idx];
+__device__ __forceinline__ void load_bias_raw(ChunkRaw& c, const float* __restrict__ bias,
+                                              int64_t begin, int64_t end, int ci, int lane,
+                                              int zrow) {
+  if (!USER) {
+    const bool ok = begin + 64 * (int64_t)ci + lane < end;
+    c.b = bias[ok ? c.idx : zrow];
+  }
 }
 
-__device__ __forceinline__ ChunkRegs finish_chunk(const ChunkRaw& c) {
+__device__ __forceinline__ ChunkRegs finish_raw(const ChunkRaw& c, int64_t begin, int64_t end,
+                                                int ci, int lane, int zrow) {
+  const bool ok = begin + 64 * (int64_t)ci + lane < end;
   ChunkRegs r;
-  r.idx = c.idx;
-  r.w = c.r - c.b;
+  r.idx = ok ? c.idx : zrow;
+  r.w = ok ? c.r - c.b : 0.f;
   return r;
 }
 
@@ -575,6 +584,12 @@ __device__ __forceinline__ void gather_group(float (&a)[G][NB], float (&ww)[G], 
 #endif
     ww[u] = __shfl(cr.w, src, 64);
     const char* p = Fc + (uint64_t)(uint32_t)ri * row_bytes;
+#if defined(MR_GRAM_PROBE) && MR_GRAM_PROBE == 3
+    // probe: no gathers (operands derived from the chunk registers)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) a[u][b] = __int_as_float(ri) * (float)(b + 1);
+    continue;
+#endif
     if constexpr (NB % 4 == 0) {
 #pragma unroll
       for (int h = 0; h < NB / 4; ++h) {
@@ -603,9 +618,13 @@ __device__ __forceinline__ void mfma_group(floatx4 (&acc)[NB * (NB + 1) / 2],
                                            float (&cacc)[NB], float (&sacc)[NB], float& wsum,
                                            const float (&a)[G][NB], const float (&ww)[G],
                                            int steps_left) {
+  // one scalar test per group: a partial group's missing steps gathered the
+  // all-zero row with weight 0, so their MFMAs add exact zeros (per-step
+  // tests split the group into blocks that defeat register reuse)
+  if (steps_left <= 0) return;
 #pragma unroll
   for (int u = 0; u < G; ++u) {
-    if (u < steps_left) {     // wave-uniform (scalar) test
+    {
       int t = 0;
 #pragma unroll
       for (int bi = 0; bi < NB; ++bi)
@@ -646,7 +665,6 @@ __device__ __forceinline__ void gram_wave(
   const int q = lane >> 4, col = lane & 15;
   const int64_t end = wbeg + wlen;
   const int nst = (wlen + 3) >> 2;              // steps of 4 ratings
-  const int ngroups = (nst + G - 1) / G;
   const uint32_t row_bytes = (uint32_t)ldk * 4u;
   const char* Fc = reinterpret_cast<const char*>(F) + 4 * NB * col;
 
@@ -668,35 +686,53 @@ __device__ __forceinline__ void gram_wave(
   for (int b = 0; b < NB; ++b) { cacc[b] = 0.f; sacc[b] = 0.f; }
   float wsum = 0.f;
 
-  // Software pipeline over groups of G steps: while group g's MFMAs run,
-  // the rows of group g+1 are in flight (buffers A/B alternate).  Every
-  // gather is unconditional (slots past the end read the zero row), so the
-  // loads land directly in the buffer registers without merge copies; only
-  // the chunk registers rotate, once per 64 ratings, under a scalar branch.
-  // chunk pipeline: cur (in use), nxt (ids, ratings and bias loaded), nx2
-  // (ids and ratings loaded; its bias gather is issued at the next rotation)
-  float aA[G][NB], wA[G], aB[G][NB], wB[G];
-  ChunkRaw c0 = load_chunk(idx, val, wbeg, end, 0, lane, zrow);
-  ChunkRaw nxt = load_chunk(idx, val, wbeg, end, 1, lane, zrow);
-  ChunkRaw nx2 = load_chunk(idx, val, wbeg, end, 2, lane, zrow);
-  load_bias<USER>(c0, bias);
-  load_bias<USER>(nxt, bias);
-  ChunkRegs cur = finish_chunk(c0);
-  int nchunk = 3;   // index of the next chunk to load
-  auto rotate = [&]() {
-    cur = finish_chunk(nxt);
+  // Chunk pipeline (64 ratings per chunk): cur (in use), nxt (ids, ratings
+  // and bias loaded), nx2 (ids and ratings loaded; its bias gather is issued
+  // when it becomes nxt).  Raw loads are masked only when their chunk
+  // becomes current, so no select waits on a load that was just issued.
+  // Every row gather is unconditional (slots past the end read the zero
+  // row), so loads land directly in the buffer registers without merges.
+  const int64_t safe = wlen > 0 ? wbeg : 0;    // an address every wave may read
+  ChunkRaw c0 = load_chunk_raw(idx, val, wbeg, end, safe, 0, lane);
+  ChunkRaw nxt = load_chunk_raw(idx, val, wbeg, end, safe, 1, lane);
+  ChunkRaw nx2 = load_chunk_raw(idx, val, wbeg, end, safe, 2, lane);
+  load_bias_raw<USER>(c0, bias, wbeg, end, 0, lane, zrow);
+  load_bias_raw<USER>(nxt, bias, wbeg, end, 1, lane, zrow);
+  ChunkRegs cur = finish_raw(c0, wbeg, end, 0, lane, zrow);
+  // One loop iteration = one chunk (GPC groups).  NBUF row buffers, group j
+  // of a chunk in buffer j % NBUF (NBUF divides GPC, so the mapping is the
+  // same every chunk and nothing is copied at the back-edge); the rows of
+  // group j + NBUF - 1 are gathered while group j's MFMAs run, so NBUF - 1
+  // groups are in flight.
+  constexpr int NBUF = (MR_GRAM_NBUF < GPC) ? MR_GRAM_NBUF : GPC;
+  constexpr int DIST = NBUF - 1;
+  static_assert(GPC % NBUF == 0, "buffers must tile a chunk");
+  float ab[NBUF][G][NB], wb[NBUF][G];
+#pragma unroll
+  for (int j = 0; j < DIST; ++j) gather_group<NB, G>(ab[j], wb[j], cur, j * G, Fc, row_bytes, q);
+  const int nchunks = (wlen + 63) >> 6;
+  for (int c = 0; c < nchunks; ++c) {
+    ChunkRegs nxtr = cur;
+#pragma unroll
+    for (int j = 0; j < GPC; ++j) {
+      const int jn = j + DIST;   // group gathered now (>= GPC: next chunk)
+      if (jn < GPC) {
+        gather_group<NB, G>(ab[jn % NBUF], wb[jn % NBUF], cur, jn * G, Fc, row_bytes, q);
+      } else {
+        if (jn == GPC) nxtr = finish_raw(nxt, wbeg, end, c + 1, lane, zrow);
+        gather_group<NB, G>(ab[jn % NBUF], wb[jn % NBUF], nxtr, (jn - GPC) * G, Fc, row_bytes,
+                            q);
+      }
+      mfma_group<NB, G, USER>(acc, cacc, sacc, wsum, ab[j % NBUF], wb[j % NBUF],
+                              nst - (c * GPC + j) * G);
+      // this buffer is dead from here: keep its last readers (the rhs FMAs)
+      // above its refill, so the refill reuses its registers
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    cur = nxtr;
     nxt = nx2;
-    load_bias<USER>(nxt, bias);
-    nx2 = load_chunk(idx, val, wbeg, end, nchunk++, lane, zrow);
-  };
-  gather_group<NB, G>(aA, wA, cur, 0, Fc, row_bytes, q);
-  for (int g = 0; g < ngroups; g += 2) {
-    if ((g + 1) % GPC == 0) rotate();
-    gather_group<NB, G>(aB, wB, cur, ((g + 1) % GPC) * G, Fc, row_bytes, q);
-    mfma_group<NB, G, USER>(acc, cacc, sacc, wsum, aA, wA, nst - g * G);
-    if ((g + 2) % GPC == 0) rotate();
-    gather_group<NB, G>(aA, wA, cur, ((g + 2) % GPC) * G, Fc, row_bytes, q);
-    mfma_group<NB, G, USER>(acc, cacc, sacc, wsum, aB, wB, nst - (g + 1) * G);
+    load_bias_raw<USER>(nxt, bias, wbeg, end, c + 2, lane, zrow);
+    nx2 = load_chunk_raw(idx, val, wbeg, end, safe, c + 3, lane);
   }
 
   // ---- epilogue -----------------------------------------------------------
@@ -776,11 +812,8 @@ __device__ __forceinline__ void gram_wave(
 // the FUSE form, whose waves then start the CG solve on their entity
 // (cg_start_entity; split entities are started after slab_reduce) and meet
 // once at the end to store the block's (r.r, p.Gp) pair.
-#ifndef MR_GRAM_WPE
-#define MR_GRAM_WPE 1
-#endif
 template <int NB, int G, bool USER, bool NTS, bool FUSE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MR_GRAM_WPE))) void gram_kernel(
+__global__ __launch_bounds__(256) void gram_kernel(
     const WorkItem* __restrict__ work, int64_t n_work,
     const int32_t* __restrict__ idx, const float* __restrict__ val,
     const float* __restrict__ F, const float* __restrict__ bias, int k, int ldk, int zrow,
@@ -842,8 +875,9 @@ static int launch_gram_g(hipStream_t s, bool user_side, int k, const WorkItem* w
 }
 
 // Pipeline group size G (steps of 4 ratings gathered per buffer).  Measured
-// on MI355X (tools/gram_bench.py, ML-full shape): G = 4 is best or within 2 %
-// for k = 32, 64, 128; MR_GRAM_G=2|4|8 overrides (tuning).
+// on MI355X (tools/ab_variants.sh, ML-full shape, k = 64): G = 2 with 4
+// buffers is best (Gram 926 / 830 us vs 959 / 858 with G = 4, 2 buffers);
+// MR_GRAM_G=2|4|8 overrides (tuning).
 static int gram_group_size(int nb) {
   static int env = -2;
   if (env == -2) {
@@ -851,7 +885,7 @@ static int gram_group_size(int nb) {
     env = e ? atoi(e) : -1;
   }
   if (env == 2 || env == 4 || env == 8) return env;
-  return 4;
+  return 2;
 }
 
 template <int NB>
