@@ -16,4 +16,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_fetch -o run --output-format csv -- python3 bench.py --no-cpu --steps 3 --warmup 1 > /dev/null 2> $OUT/pmc_fetch.err || { echo "PMC FETCH FAILED"; tail -20 $OUT/pmc_fetch.err; exit 1; }
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/pmc_write -o run --output-format csv -- python3 bench.py --no-cpu --steps 3 --warmup 1 > /dev/null 2> $OUT/pmc_write.err || { echo "PMC WRITE FAILED"; tail -20 $OUT/pmc_write.err; exit 1; }
 python tools/pmc_summary.py --fetch $OUT/pmc_fetch --write $OUT/pmc_write --out $OUT/pmc.json
+
+timeout -k 10 600 python bench.py --no-cpu --k 128 --steps 20 > $OUT/bench_k128.json 2> $OUT/bench_k128.err || { echo "K128 BENCH FAILED"; tail -20 $OUT/bench_k128.err; exit 1; }
+echo K128; cat $OUT/bench_k128.json
 echo DONE
