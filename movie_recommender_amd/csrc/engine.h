@@ -60,6 +60,8 @@ struct Engine {
   CgState* h_state = nullptr;
   CgState* h_init = nullptr;
   double* h_stage = nullptr;
+  double* h_fac = nullptr;   // pinned factor staging (set/get_factors)
+  int64_t h_fac_n = 0;
   CgMirror* h_mirror = nullptr;   // pinned, host-mapped, coherent
   CgMirror* d_mirror = nullptr;   // its device address
   int mirror_seq = 0;
@@ -71,6 +73,7 @@ struct Engine {
   int chunk = 2048;
   bool fuse_start = true;   // CG start in the Gram epilogue (MR_FUSE_START=0: off)
   bool timing = false;
+  hipEvent_t hs_event = nullptr;   // half-step boundary marker (debug)
   std::vector<hipEvent_t> ev_pool;
   std::vector<Pending> pending;
   std::vector<PhaseSpan> spans;
@@ -91,6 +94,7 @@ struct Engine {
                  const int32_t* d_other, const double* d_r);
   int set_factors(const double* hU, const double* hV);
   int get_factors(double* hU, double* hV);
+  int fac_stage(int64_t n);
   // RCCL attached (any world size, so the collective path is exercised even
   // single-rank) or host callbacks with more than one rank.
   bool sharded() const { return rccl != nullptr || (has_comm && comm.world > 1); }

@@ -65,8 +65,10 @@ Engine::~Engine() {
     if (h_state) (void)hipHostFree(h_state);
     if (h_init) (void)hipHostFree(h_init);
     if (h_stage) (void)hipHostFree(h_stage);
+    if (h_fac) (void)hipHostFree(h_fac);
     if (h_mirror) (void)hipHostFree(h_mirror);
     for (auto& e : ev_pool) (void)hipEventDestroy(e);
+    if (hs_event) (void)hipEventDestroy(hs_event);
     for (auto& p : pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto& sp : spans) if (sp.end) (void)hipEventDestroy(sp.end);
     if (rccl) (void)ncclCommDestroy((ncclComm_t)rccl);
@@ -320,43 +322,91 @@ int Engine::init(int dev, int k_, int64_t U_, int64_t I_, int64_t n_u,
 // ----------------------------------------------------------------------------
 // factors
 // ----------------------------------------------------------------------------
+// Factor transfers stage through pinned host memory that the pack / unpack
+// kernels read and write directly (zero-copy; fine-grained, system-coherent).
+// The earlier form -- a pageable hipMemcpyAsync into a pool buffer, then a
+// kernel -- let replays from one snapshot diverge run to run (a kernel saw
+// stale staging data).  MR_XFER_DMA=1 restores it for A/B checks.
+static bool xfer_dma() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MR_XFER_DMA");
+    v = (e && atoi(e) == 1) ? 1 : 0;
+  }
+  return v == 1;
+}
+
+int Engine::fac_stage(int64_t n) {
+  if (n <= h_fac_n) return 0;
+  if (h_fac) MR_HIP(hipHostFree(h_fac));
+  h_fac = nullptr;
+  h_fac_n = 0;
+  MR_HIP(hipHostMalloc((void**)&h_fac, (size_t)n * sizeof(double), hipHostMallocDefault));
+  h_fac_n = n;
+  return 0;
+}
+
 int Engine::set_factors(const double* hU, const double* hV) {
   MR_HIP(hipSetDevice(device));
-  double* tmp = nullptr;
-  const int64_t nmax = std::max(U * (k + 1), I * (int64_t)k);
-  if (dalloc(&tmp, nmax, stream)) return -1;
+  const int64_t nU = U * (k + 1), nV = I * (int64_t)k;
   int rc = 0;
+  if (xfer_dma()) {
+    double* tmp = nullptr;
+    if (dalloc(&tmp, nU + nV, stream)) return -1;
+    if (hU && U) {
+      MR_HIP(hipMemcpyAsync(tmp, hU, nU * 8, hipMemcpyHostToDevice, stream));
+      rc |= launch_unpack_factors(stream, U, k + 1, k, ldk, tmp, Ufac, Ubias);
+    }
+    if (hV && I) {
+      MR_HIP(hipMemcpyAsync(tmp + nU, hV, nV * 8, hipMemcpyHostToDevice, stream));
+      rc |= launch_unpack_factors(stream, I, k, k, ldk, tmp + nU, Vfac, nullptr);
+    }
+    MR_HIP(hipStreamSynchronize(stream));
+    dfree(tmp, stream);
+    return rc ? -1 : 0;
+  }
+  MR_HIP(hipStreamSynchronize(stream));   // no kernel may still read h_fac
+  if (fac_stage(nU + nV)) return -1;
   if (hU && U) {
-    MR_HIP(hipMemcpyAsync(tmp, hU, U * (k + 1) * 8, hipMemcpyHostToDevice, stream));
-    rc |= launch_unpack_factors(stream, U, k + 1, k, ldk, tmp, Ufac, Ubias);
+    memcpy(h_fac, hU, nU * 8);
+    rc |= launch_unpack_factors(stream, U, k + 1, k, ldk, h_fac, Ufac, Ubias);
   }
   if (hV && I) {
-    MR_HIP(hipMemcpyAsync(tmp, hV, I * (int64_t)k * 8, hipMemcpyHostToDevice, stream));
-    rc |= launch_unpack_factors(stream, I, k, k, ldk, tmp, Vfac, nullptr);
+    memcpy(h_fac + nU, hV, nV * 8);
+    rc |= launch_unpack_factors(stream, I, k, k, ldk, h_fac + nU, Vfac, nullptr);
   }
   MR_HIP(hipStreamSynchronize(stream));
-  dfree(tmp, stream);
   return rc ? -1 : 0;
 }
 
 int Engine::get_factors(double* hU, double* hV) {
   MR_HIP(hipSetDevice(device));
-  double* tmp = nullptr;
-  const int64_t nmax = std::max(U * (k + 1), I * (int64_t)k);
-  if (dalloc(&tmp, nmax, stream)) return -1;
+  const int64_t nU = U * (k + 1), nV = I * (int64_t)k;
   int rc = 0;
-  if (hU && U) {
-    rc |= launch_pack_factors(stream, U, k + 1, k, ldk, Ufac, Ubias, tmp);
-    MR_HIP(hipMemcpyAsync(hU, tmp, U * (k + 1) * 8, hipMemcpyDeviceToHost, stream));
+  if (xfer_dma()) {
+    double* tmp = nullptr;
+    if (dalloc(&tmp, std::max(nU, nV), stream)) return -1;
+    if (hU && U) {
+      rc |= launch_pack_factors(stream, U, k + 1, k, ldk, Ufac, Ubias, tmp);
+      MR_HIP(hipMemcpyAsync(hU, tmp, nU * 8, hipMemcpyDeviceToHost, stream));
+      MR_HIP(hipStreamSynchronize(stream));
+    }
+    if (hV && I) {
+      rc |= launch_pack_factors(stream, I, k, k, ldk, Vfac, nullptr, tmp);
+      MR_HIP(hipMemcpyAsync(hV, tmp, nV * 8, hipMemcpyDeviceToHost, stream));
+      MR_HIP(hipStreamSynchronize(stream));
+    }
+    dfree(tmp, stream);
     MR_HIP(hipStreamSynchronize(stream));
+    return rc ? -1 : 0;
   }
-  if (hV && I) {
-    rc |= launch_pack_factors(stream, I, k, k, ldk, Vfac, nullptr, tmp);
-    MR_HIP(hipMemcpyAsync(hV, tmp, I * (int64_t)k * 8, hipMemcpyDeviceToHost, stream));
-    MR_HIP(hipStreamSynchronize(stream));
-  }
-  dfree(tmp, stream);
   MR_HIP(hipStreamSynchronize(stream));
+  if (fac_stage(nU + nV)) return -1;
+  if (hU && U) rc |= launch_pack_factors(stream, U, k + 1, k, ldk, Ufac, Ubias, h_fac);
+  if (hV && I) rc |= launch_pack_factors(stream, I, k, k, ldk, Vfac, nullptr, h_fac + nU);
+  MR_HIP(hipStreamSynchronize(stream));
+  if (hU && U) memcpy(hU, h_fac, nU * 8);
+  if (hV && I) memcpy(hV, h_fac + nU, nV * 8);
   return rc ? -1 : 0;
 }
 
@@ -476,7 +526,12 @@ int Engine::wait_mirror(int target, CgMirror* out) {
       if (__atomic_load_n(&h_mirror->seq, __ATOMIC_ACQUIRE) == cur) return 0;
       continue;  // a newer state landed while copying: read again
     }
-    if ((++spins & 1023) == 0) {
+    static int noq = -1;   // debug: MR_NO_QUERY=1 never queries the stream
+    if (noq < 0) {
+      const char* e = getenv("MR_NO_QUERY");
+      noq = (e && atoi(e) == 1) ? 1 : 0;
+    }
+    if (!noq && (++spins & 1023) == 0) {
       const hipError_t q = hipStreamQuery(stream);
       if (q == hipSuccess) {
         if (__atomic_load_n(&h_mirror->seq, __ATOMIC_ACQUIRE) >= target) continue;
@@ -657,8 +712,13 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr, bool start
   // only after two stagnating steps, so both are enqueued behind the init
   // without waiting for its state (they are no-ops if the init already
   // finished the solve: rr < 1e-6 or max_it == 0).
+  static int spec = -1;     // MR_CG_SPEC=0: no speculative launches (debug)
+  if (spec < 0) {
+    const char* e = getenv("MR_CG_SPEC");
+    spec = (e && atoi(e) == 0) ? 0 : 1;
+  }
   int launched = 0;          // iterations enqueued so far
-  for (; launched < std::min(2, max_it); ++launched)
+  for (; launched < std::min(spec ? 2 : 1, max_it); ++launched)
     if (launch_iter(launched)) return -1;
   CgMirror ms{};
   if (wait_mirror(seq_init, &ms)) return -1;
@@ -669,7 +729,7 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr, bool start
       ++launched;
     }
     // speculate one further iteration when iteration known+1 cannot stop
-    if (launched == known + 2 && ms.fails == 0 && ms.rr > 1e-4 && known + 2 < max_it) {
+    if (spec && launched == known + 2 && ms.fails == 0 && ms.rr > 1e-4 && known + 2 < max_it) {
       if (launch_iter(launched)) return -1;
       ++launched;
     }
@@ -716,6 +776,19 @@ int Engine::half_step(bool user, double min_dec, int max_it, double* final_rr) {
     if (solve(S)) return -1;
   }
   if (allgather_side(user)) return -1;
+  {
+    static int hsm = -1;   // debug: MR_HS_MARKER = 1 marker event, 2 stream sync
+    if (hsm < 0) {
+      const char* e = getenv("MR_HS_MARKER");
+      hsm = e ? atoi(e) : 0;
+    }
+    if (hsm == 1) {
+      if (!hs_event) MR_HIP(hipEventCreate(&hs_event));
+      MR_HIP(hipEventRecord(hs_event, stream));
+    } else if (hsm == 2) {
+      MR_HIP(hipStreamSynchronize(stream));
+    }
+  }
   if (timing) {
     hipEvent_t end = nullptr;
     if (sharded()) {   // the RCCL exchange belongs to the solve phase

@@ -20,6 +20,9 @@
 // Tuning switch (build-time; tools/build_variant.sh): row buffers of the
 // Gram main loop (groups in flight + 1).  Measured on MI355X (ML-full shape,
 // k = 64, tools/ab_gram.sh): 4 buffers of G = 2 steps is best.
+#ifndef MR_BF3_ORDER
+#define MR_BF3_ORDER 0   // bf16x3 MFMA order: 0 product-major, 1 block-major
+#endif
 #ifndef MR_GRAM_NBUF
 #define MR_GRAM_NBUF 4
 #endif
@@ -647,6 +650,114 @@ __device__ __forceinline__ void mfma_group(floatx4 (&acc)[NB * (NB + 1) / 2],
   }
 }
 
+// ---- bf16x3 main loop pieces --------------------------------------------
+// v_mfma_f32_16x16x32_bf16 takes, in lane (q, col), 8 consecutive K values of
+// row / column col.  With K = ratings that is "ratings 8q .. 8q+7 of virtual
+// column 16b + col", which is what lane (q, col) holds after gathering rows
+// 8q + t (t < 8) of a 32-rating half with its NB-float segment per row (the
+// f32 kernel's gather, 8 rows per lane instead of 1 per step): the operands
+// need no transpose.  Each float is split EXACTLY into three bf16 by
+// truncation (h = top 16 bits, m = top 16 bits of a - h, l = a - h - m, which
+// has <= 8 significant bits), and each block accumulates the six products of
+// weight >= 2^-16 of h h^T: hh + hm + mh + hl + lh + mm (dropped ml, lm, ll
+// are <= 2^-24 relative, below fp32 rounding of the sum).
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+template <int NB>
+__device__ __forceinline__ void gather_half(float (&f)[8][NB], float (&w)[8], ChunkRegs cr,
+                                            int half, const char* __restrict__ Fc,
+                                            uint32_t row_bytes, int q) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int src = 32 * half + 8 * q + t;
+    const int ri = __shfl(cr.idx, src, 64);
+    w[t] = __shfl(cr.w, src, 64);
+#if defined(MR_GRAM_PROBE) && MR_GRAM_PROBE == 3
+#pragma unroll
+    for (int b = 0; b < NB; ++b) f[t][b] = __int_as_float(ri) * (float)(b + 1);
+    continue;
+#endif
+    load_row_seg<NB>(f[t], reinterpret_cast<const float*>(Fc + (uint64_t)(uint32_t)ri * row_bytes));
+  }
+}
+
+// rhs c = sum a w and (user side) row sums, fp32 on VALU, per lane over its
+// 8 ratings (the 4 q-groups are combined in the epilogue); then the exact
+// 3-way split, packed 2 ratings per dword (rating 2j in the low half).
+template <int NB, bool USER>
+__device__ __forceinline__ void bf3_split(u32x4_t (&P)[3][NB], float (&cacc)[NB],
+                                          float (&sacc)[NB], float& wsum,
+                                          const float (&f)[8][NB], const float (&w)[8]) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      cacc[b] = fmaf(f[t][b], w[t], cacc[b]);
+      if (USER) sacc[b] += f[t][b];
+    }
+    if (USER) wsum += w[t];
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x2_t x = {f[2 * j][b], f[2 * j + 1][b]};
+      const u32x2_t xa = __builtin_bit_cast(u32x2_t, x);
+      const f32x2_t r = x - __builtin_bit_cast(f32x2_t, xa & 0xFFFF0000u);   // v_pk_add_f32
+      const u32x2_t ra = __builtin_bit_cast(u32x2_t, r);
+      const f32x2_t sv = r - __builtin_bit_cast(f32x2_t, ra & 0xFFFF0000u);
+      const u32x2_t sa = __builtin_bit_cast(u32x2_t, sv);
+      P[0][b][j] = __builtin_amdgcn_perm(xa[1], xa[0], 0x07060302u);
+      P[1][b][j] = __builtin_amdgcn_perm(ra[1], ra[0], 0x07060302u);
+      P[2][b][j] = __builtin_amdgcn_perm(sa[1], sa[0], 0x07060302u);
+    }
+  }
+}
+
+// hh, hm, mh, hl, lh, mm over the NB(NB+1)/2 upper blocks
+template <int NB>
+__device__ __forceinline__ void bf3_mfma(floatx4 (&acc)[NB * (NB + 1) / 2],
+                                         const u32x4_t (&P)[3][NB]) {
+#if MR_BF3_ORDER == 0
+#pragma unroll
+  for (int sidx = 0; sidx < 6; ++sidx) {
+    const int pa = (sidx == 2) ? 1 : (sidx == 4) ? 2 : (sidx == 5) ? 1 : 0;
+    const int pb = (sidx == 1) ? 1 : (sidx == 3) ? 2 : (sidx == 5) ? 1 : 0;
+    int t = 0;
+#pragma unroll
+    for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+      for (int bj = bi; bj < NB; ++bj) {
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            __builtin_bit_cast(bf16x8_t, P[pa][bi]), __builtin_bit_cast(bf16x8_t, P[pb][bj]),
+            acc[t], 0, 0, 0);
+        ++t;
+      }
+  }
+#else
+  int t = 0;
+#pragma unroll
+  for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+    for (int bj = bi; bj < NB; ++bj) {
+      floatx4 a = acc[t];
+#pragma unroll
+      for (int sidx = 0; sidx < 6; ++sidx) {
+        const int pa = (sidx == 2) ? 1 : (sidx == 4) ? 2 : (sidx == 5) ? 1 : 0;
+        const int pb = (sidx == 1) ? 1 : (sidx == 3) ? 2 : (sidx == 5) ? 1 : 0;
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, P[pa][bi]),
+                                                    __builtin_bit_cast(bf16x8_t, P[pb][bj]), a,
+                                                    0, 0, 0);
+      }
+      acc[t] = a;
+      ++t;
+    }
+#endif
+}
+
 template <int NB, int G, bool USER, bool NTS, bool FUSE>
 __device__ __forceinline__ void gram_wave(
     int64_t wi, const WorkItem* __restrict__ work,
@@ -655,7 +766,8 @@ __device__ __forceinline__ void gram_wave(
     const GramDst& direct, const GramDst& slab, const CgStart& cs, StartScratch<NB>* ssc,
     double& drr, double& dpq) {
   constexpr int T = NB * (NB + 1) / 2;
-  constexpr int GPC = 16 / G;              // groups per 64-rating chunk
+  constexpr bool BF3 = (G == 0);           // bf16x3 matrix-core path
+  constexpr int GPC = BF3 ? 2 : 16 / G;    // groups per 64-rating chunk
   const int lane = threadIdx.x & 63;
   // work-item fields in SGPRs: all control flow below is scalar
   const int64_t wbeg = work[wi].begin;
@@ -699,6 +811,7 @@ __device__ __forceinline__ void gram_wave(
   load_bias_raw<USER>(c0, bias, wbeg, end, 0, lane, zrow);
   load_bias_raw<USER>(nxt, bias, wbeg, end, 1, lane, zrow);
   ChunkRegs cur = finish_raw(c0, wbeg, end, 0, lane, zrow);
+  if constexpr (!BF3) {
   // One loop iteration = one chunk (GPC groups).  NBUF row buffers, group j
   // of a chunk in buffer j % NBUF (NBUF divides GPC, so the mapping is the
   // same every chunk and nothing is copied at the back-edge); the rows of
@@ -707,9 +820,10 @@ __device__ __forceinline__ void gram_wave(
   constexpr int NBUF = (MR_GRAM_NBUF < GPC) ? MR_GRAM_NBUF : GPC;
   constexpr int DIST = NBUF - 1;
   static_assert(GPC % NBUF == 0, "buffers must tile a chunk");
-  float ab[NBUF][G][NB], wb[NBUF][G];
+  constexpr int GG = BF3 ? 1 : G;
+  float ab[NBUF][GG][NB], wb[NBUF][GG];
 #pragma unroll
-  for (int j = 0; j < DIST; ++j) gather_group<NB, G>(ab[j], wb[j], cur, j * G, Fc, row_bytes, q);
+  for (int j = 0; j < DIST; ++j) gather_group<NB, GG>(ab[j], wb[j], cur, j * GG, Fc, row_bytes, q);
   const int nchunks = (wlen + 63) >> 6;
   for (int c = 0; c < nchunks; ++c) {
     ChunkRegs nxtr = cur;
@@ -717,14 +831,14 @@ __device__ __forceinline__ void gram_wave(
     for (int j = 0; j < GPC; ++j) {
       const int jn = j + DIST;   // group gathered now (>= GPC: next chunk)
       if (jn < GPC) {
-        gather_group<NB, G>(ab[jn % NBUF], wb[jn % NBUF], cur, jn * G, Fc, row_bytes, q);
+        gather_group<NB, GG>(ab[jn % NBUF], wb[jn % NBUF], cur, jn * GG, Fc, row_bytes, q);
       } else {
         if (jn == GPC) nxtr = finish_raw(nxt, wbeg, end, c + 1, lane, zrow);
-        gather_group<NB, G>(ab[jn % NBUF], wb[jn % NBUF], nxtr, (jn - GPC) * G, Fc, row_bytes,
-                            q);
+        gather_group<NB, GG>(ab[jn % NBUF], wb[jn % NBUF], nxtr, (jn - GPC) * GG, Fc,
+                             row_bytes, q);
       }
-      mfma_group<NB, G, USER>(acc, cacc, sacc, wsum, ab[j % NBUF], wb[j % NBUF],
-                              nst - (c * GPC + j) * G);
+      mfma_group<NB, GG, USER>(acc, cacc, sacc, wsum, ab[j % NBUF], wb[j % NBUF],
+                               nst - (c * GPC + j) * GG);
       // this buffer is dead from here: keep its last readers (the rhs FMAs)
       // above its refill, so the refill reuses its registers
       __builtin_amdgcn_sched_barrier(0);
@@ -733,6 +847,61 @@ __device__ __forceinline__ void gram_wave(
     nxt = nx2;
     load_bias_raw<USER>(nxt, bias, wbeg, end, c + 2, lane, zrow);
     nx2 = load_chunk_raw(idx, val, wbeg, end, safe, c + 3, lane);
+  }
+
+  } else {
+    // bf16x3 main loop: one iteration = one 32-rating half with its own
+    // id / weight registers (lanes 0..31; lanes 32..63 mirror them), so the
+    // loop body is uniform: ONE split site and ONE MFMA site (two call sites
+    // per iteration made the compiler rotate the accumulators through extra
+    // AGPRs every iteration).  The half's rows land in F; once split into P
+    // (and the rhs taken), F is refilled with the next half while P's 60
+    // MFMAs run.  Rows past the end are the zero row with weight 0.
+    auto ld32 = [&](int c) {
+      const int64_t jj = wbeg + 32 * (int64_t)c + (lane & 31);
+      ChunkRaw r;
+      const int64_t js = jj < end ? jj : safe;
+      r.idx = idx[js];
+      r.r = val[js];
+      r.b = 0.f;
+      return r;
+    };
+    auto bias32 = [&](ChunkRaw& cr, int c) {
+      if (!USER) {
+        const bool ok = wbeg + 32 * (int64_t)c + (lane & 31) < end;
+        cr.b = bias[ok ? cr.idx : zrow];
+      }
+    };
+    auto fin32 = [&](const ChunkRaw& cr, int c) {
+      const bool ok = wbeg + 32 * (int64_t)c + (lane & 31) < end;
+      ChunkRegs r;
+      r.idx = ok ? cr.idx : zrow;
+      r.w = ok ? cr.r - cr.b : 0.f;
+      return r;
+    };
+    // Per iteration: gather half h+1 into F, run half h's MFMAs from P, then
+    // split F into P.  F is loaded and consumed inside one iteration and only
+    // VALU results (P) cross the back-edge, so no register copy there ever
+    // waits on a load in flight.
+    ChunkRaw h1 = ld32(1), h2 = ld32(2);
+    ChunkRaw h0 = ld32(0);
+    bias32(h0, 0);
+    bias32(h1, 1);
+    float F[8][NB], w[8];
+    u32x4_t P[3][NB];
+    gather_half<NB>(F, w, fin32(h0, 0), 0, Fc, row_bytes, q);
+    bf3_split<NB, USER>(P, cacc, sacc, wsum, F, w);
+    const int nhalves = (wlen + 31) >> 5;
+    for (int h = 0; h < nhalves; ++h) {
+      const ChunkRaw h3 = ld32(h + 3);
+      bias32(h2, h + 2);
+      gather_half<NB>(F, w, fin32(h1, h + 1), 0, Fc, row_bytes, q);
+      bf3_mfma<NB>(acc, P);
+      __builtin_amdgcn_sched_barrier(0);
+      bf3_split<NB, USER>(P, cacc, sacc, wsum, F, w);
+      h1 = h2;
+      h2 = h3;
+    }
   }
 
   // ---- epilogue -----------------------------------------------------------
@@ -882,9 +1051,10 @@ static int gram_group_size(int nb) {
   static int env = -2;
   if (env == -2) {
     const char* e = getenv("MR_GRAM_G");
-    env = e ? atoi(e) : -1;
+    const char* b = getenv("MR_GRAM_BF3");
+    env = (b && atoi(b) == 0) ? (e ? atoi(e) : 2) : 0;
   }
-  if (env == 2 || env == 4 || env == 8) return env;
+  if (env == 0 || env == 2 || env == 4) return env;
   return 2;
 }
 
@@ -895,9 +1065,9 @@ static int launch_gram_nb(hipStream_t s, bool user_side, int k, const WorkItem* 
                           GramDst slab, const CgStart* start) {
   if (n_work <= 0) return 0;
   switch (gram_group_size(NB)) {
-    case 2: return launch_gram_g<NB, 2>(s, user_side, k, work, n_work, idx, val, F, bias, zrow, direct, slab, start);
+    case 0: return launch_gram_g<NB, 0>(s, user_side, k, work, n_work, idx, val, F, bias, zrow, direct, slab, start);
     case 4: return launch_gram_g<NB, 4>(s, user_side, k, work, n_work, idx, val, F, bias, zrow, direct, slab, start);
-    default: return launch_gram_g<NB, 8>(s, user_side, k, work, n_work, idx, val, F, bias, zrow, direct, slab, start);
+    default: return launch_gram_g<NB, 2>(s, user_side, k, work, n_work, idx, val, F, bias, zrow, direct, slab, start);
   }
 }
 
@@ -1015,52 +1185,110 @@ int launch_slab_reduce(hipStream_t s, bool user_side, int k,
 // product T^T v_bi into y_bj; the 4-lane row partials and 16-lane column
 // partials are combined once per entity through LDS in a fixed order.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void publish(const CgState* st, CgMirror* m, int seq) {
+// The CG state is shared by every block of consecutive kernels running on
+// all 8 XCDs, whose L2s are not coherent with each other: every kernel reads
+// it with agent-scope (sc1) loads and the single finalizing thread writes it
+// with agent-scope stores, so no block ever sees a line its XCD's L2 cached
+// before the previous kernel updated it.  (Plain accesses made replays of the
+// same steps diverge depending on launch timing.)
+template <class T>
+__device__ __forceinline__ T ald(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ void ast(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+struct CgScalars {   // the fields the rules read and write
+  double rr, alpha, beta, final_rr, min_dec, comm0, comm1;
+  int32_t it, fails, done, ret, max_it, n_matvec, sharded;
+};
+__device__ __forceinline__ CgScalars load_state(const CgState* st) {
+  CgScalars v;
+  v.rr = ald(&st->rr);
+  v.alpha = ald(&st->alpha);
+  v.beta = ald(&st->beta);
+  v.final_rr = ald(&st->final_rr);
+  v.min_dec = ald(&st->min_dec);
+  v.comm0 = ald(&st->comm[0]);
+  v.comm1 = ald(&st->comm[1]);
+  v.it = ald(&st->it);
+  v.fails = ald(&st->fails);
+  v.done = ald(&st->done);
+  v.ret = ald(&st->ret);
+  v.max_it = ald(&st->max_it);
+  v.n_matvec = ald(&st->n_matvec);
+  v.sharded = ald(&st->sharded);
+  return v;
+}
+__device__ __forceinline__ void store_state(CgState* st, const CgScalars& v) {
+  ast(&st->rr, v.rr);
+  ast(&st->alpha, v.alpha);
+  ast(&st->beta, v.beta);
+  ast(&st->final_rr, v.final_rr);
+  ast(&st->min_dec, v.min_dec);
+  ast(&st->comm[0], v.comm0);
+  ast(&st->comm[1], v.comm1);
+  ast(&st->it, v.it);
+  ast(&st->fails, v.fails);
+  ast(&st->done, v.done);
+  ast(&st->ret, v.ret);
+  ast(&st->max_it, v.max_it);
+  ast(&st->n_matvec, v.n_matvec);
+  ast(&st->sharded, v.sharded);
+}
+
+__device__ __forceinline__ void publish(const CgScalars& v, CgMirror* m, int seq) {
   if (!m) return;
-  m->done = st->done;
-  m->fails = st->fails;
-  m->it = st->it;
-  m->ret = st->ret;
-  m->n_matvec = st->n_matvec;
-  m->rr = st->rr;
-  m->final_rr = st->final_rr;
+  m->done = v.done;
+  m->fails = v.fails;
+  m->it = v.it;
+  m->ret = v.ret;
+  m->n_matvec = v.n_matvec;
+  m->rr = v.rr;
+  m->final_rr = v.final_rr;
   __threadfence_system();
   __hip_atomic_store(&m->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // INIT / ALPHA / BETA rules on the reduced sum s (one thread).
 __device__ void cg_finalize(CgState* st, int phase, double s, CgMirror* mirror, int seq) {
+  CgScalars v = load_state(st);
   if (phase == CG_INIT) {
-    st->rr = s;
-    st->final_rr = s;
-    st->it = 0;
-    st->fails = 0;
-    st->done = 0;
-    st->ret = 0;
-    if (st->max_it <= 0 || s < 1e-6) st->done = 1;
-    publish(st, mirror, seq);
+    v.rr = s;
+    v.final_rr = s;
+    v.it = 0;
+    v.fails = 0;
+    v.done = 0;
+    v.ret = 0;
+    if (v.max_it <= 0 || s < 1e-6) v.done = 1;
+    store_state(st, v);
+    publish(v, mirror, seq);
   } else if (phase == CG_ALPHA) {
-    st->alpha = st->rr / s;
-    st->n_matvec += 1;
+    v.alpha = v.rr / s;
+    v.n_matvec += 1;
+    store_state(st, v);
   } else {
     const double rr2 = s;
-    st->final_rr = rr2;
-    const double beta = rr2 / st->rr;
-    st->beta = beta;
-    if (beta > 1.0 - st->min_dec) st->fails += 1;
-    else st->fails = 0;
-    if (st->fails >= 2) {
-      st->done = 1;
-      st->ret = st->it;
+    v.final_rr = rr2;
+    const double beta = rr2 / v.rr;
+    v.beta = beta;
+    if (beta > 1.0 - v.min_dec) v.fails += 1;
+    else v.fails = 0;
+    if (v.fails >= 2) {
+      v.done = 1;
+      v.ret = v.it;
     } else {
-      st->rr = rr2;
-      st->it += 1;
-      if (st->it >= st->max_it || rr2 < 1e-6) {
-        st->done = 1;
-        st->ret = st->it;
+      v.rr = rr2;
+      v.it += 1;
+      if (v.it >= v.max_it || rr2 < 1e-6) {
+        v.done = 1;
+        v.ret = v.it;
       }
     }
-    publish(st, mirror, seq);
+    store_state(st, v);
+    publish(v, mirror, seq);
   }
 }
 
@@ -1091,11 +1319,11 @@ __device__ void last_block_finalize(CgState* st, int phase, double* partials, Cg
   const double tot = block_sum_f64<256>(acc, sh);
   if (threadIdx.x == 0) {
     __hip_atomic_store(&st->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (st->sharded) {
+    if (ald(&st->sharded)) {
       // local sum for the all-reduce; the update computes alpha itself from
       // the reduced slot, so ALPHA needs no finalize step (only its count)
-      st->comm[0] = tot;
-      if (phase == CG_BETA) st->n_matvec += 1;
+      ast(&st->comm[0], tot);
+      if (phase == CG_BETA) ast(&st->n_matvec, ald(&st->n_matvec) + 1);
     } else {
       cg_finalize(st, phase, tot, mirror, seq);
     }
@@ -1111,13 +1339,13 @@ __global__ __launch_bounds__(256) void cg_matvec_kernel(
     const float* __restrict__ r, const float* __restrict__ rb,
     float* __restrict__ y, float* __restrict__ yb, double* __restrict__ partials,
     CgState* fst, int phase) {
-  if (st->done) return;
+  if (ald(&st->done)) return;
   constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2, NTILE = NO + NF + (NB & 1);
   constexpr int64_t GS = (int64_t)NTILE * 256 + NF * 16;   // == gsize_of(k)
   constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
   __shared__ MvScratch<NB> scr[MV_WAVES];
   __shared__ double sh[MV_WAVES];
-  const float beta = (float)st->beta;
+  const float beta = (float)ald(&st->beta);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   MvScratch<NB>& sc = scr[wid];
   double dsum = 0.0;
@@ -1260,11 +1488,12 @@ __global__ __launch_bounds__(256) void cg_update_kernel(
     float* __restrict__ xb, float* __restrict__ rb, float* __restrict__ pb,
     const float* __restrict__ qb, const float* __restrict__ cb,
     double* __restrict__ partials, CgState* fst, CgMirror* mirror, int seq) {
-  if (st->done) return;
+  if (ald(&st->done)) return;
   __shared__ double sh[4];
   // sharded runs: alpha = rr / (all-reduced p.Ap), the ALPHA rule inline
-  const float alpha =
-      (float)(st->sharded && mode != UPD_INIT ? st->rr / st->comm[0] : st->alpha);
+  const float alpha = (float)(ald(&st->sharded) && mode != UPD_INIT
+                                  ? ald(&st->rr) / ald(&st->comm[0])
+                                  : ald(&st->alpha));
   double acc = 0.0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1343,7 +1572,7 @@ __global__ __launch_bounds__(CTL_THREADS) void cg_control_kernel(
     CgState* __restrict__ st, int phase, int ctl,
     const double* __restrict__ partials, int n_part, CgMirror* mirror, int seq,
     double min_dec, int max_it, int sharded) {
-  if (phase != CG_INIT && phase != CG_START && st->done) return;
+  if (phase != CG_INIT && phase != CG_START && ald(&st->done)) return;
   __shared__ double sh[CTL_THREADS / 64];
   if (ctl & CTL_REDUCE) {
     if (phase == CG_START) {
@@ -1369,43 +1598,47 @@ __global__ __launch_bounds__(CTL_THREADS) void cg_control_kernel(
       __syncthreads();
       const double tb = block_sum_f64<CTL_THREADS>(b, sh);
       if (threadIdx.x == 0) {
-        st->comm[0] = ta;
-        st->comm[1] = tb;
+        ast(&st->comm[0], ta);
+        ast(&st->comm[1], tb);
       }
     } else {
       double acc = 0.0;
       for (int i = threadIdx.x; i < n_part; i += blockDim.x) acc += partials[i];
       const double tot = block_sum_f64<CTL_THREADS>(acc, sh);
-      if (threadIdx.x == 0) st->comm[0] = tot;
+      if (threadIdx.x == 0) ast(&st->comm[0], tot);
     }
   }
   if (threadIdx.x != 0 || !(ctl & CTL_FINALIZE)) return;
   if (phase == CG_START) {
     // fresh state (cg_least_squares entry), then the INIT rule on r0.r0 and,
     // unless that ended the solve, alpha of iteration 0 from p0.G p0
-    const double rr = st->comm[0], pq = st->comm[1];
-    st->min_dec = min_dec;
-    st->max_it = max_it;
-    st->sharded = sharded;
-    st->arrive = 0;
-    st->n_matvec = 0;
-    st->alpha = 0.0;
-    st->beta = 0.0;
-    st->rr = rr;
-    st->final_rr = rr;
-    st->it = 0;
-    st->fails = 0;
-    st->ret = 0;
-    st->done = (max_it <= 0 || rr < 1e-6) ? 1 : 0;
-    if (!st->done) {
-      st->alpha = rr / pq;
-      st->comm[0] = pq;      // sharded updates derive alpha as rr / comm[0]
-      st->n_matvec = 1;      // the fused iteration-0 matvec
+    CgScalars v;
+    const double rr = ald(&st->comm[0]), pq = ald(&st->comm[1]);
+    v.min_dec = min_dec;
+    v.max_it = max_it;
+    v.sharded = sharded;
+    v.n_matvec = 0;
+    v.alpha = 0.0;
+    v.beta = 0.0;
+    v.rr = rr;
+    v.final_rr = rr;
+    v.it = 0;
+    v.fails = 0;
+    v.ret = 0;
+    v.comm0 = rr;
+    v.comm1 = pq;
+    v.done = (max_it <= 0 || rr < 1e-6) ? 1 : 0;
+    if (!v.done) {
+      v.alpha = rr / pq;
+      v.comm0 = pq;      // sharded updates derive alpha as rr / comm[0]
+      v.n_matvec = 1;    // the fused iteration-0 matvec
     }
-    publish(st, mirror, seq);
+    ast(&st->arrive, 0u);
+    store_state(st, v);
+    publish(v, mirror, seq);
     return;
   }
-  cg_finalize(st, phase, st->comm[0], mirror, seq);
+  cg_finalize(st, phase, ald(&st->comm[0]), mirror, seq);
 }
 
 int launch_cg_control(hipStream_t s, CgState* st, int phase, int ctl,
@@ -1622,7 +1855,7 @@ __global__ __launch_bounds__(256) void dot_f64_kernel(const CgState* st, int64_t
                                                       const double* __restrict__ a,
                                                       const double* __restrict__ b,
                                                       double* __restrict__ partials) {
-  if (st && st->done) return;
+  if (st && ald(&st->done)) return;
   __shared__ double sh[4];
   double acc = 0.0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -1643,9 +1876,9 @@ __global__ __launch_bounds__(256) void update_f64_kernel(
     const CgState* __restrict__ st, int mode, int64_t n, double* __restrict__ x,
     double* __restrict__ r, double* __restrict__ p, const double* __restrict__ q,
     const double* __restrict__ c, double* __restrict__ partials) {
-  if (st->done) return;
+  if (ald(&st->done)) return;
   __shared__ double sh[4];
-  const double alpha = st->alpha;
+  const double alpha = ald(&st->alpha);
   double acc = 0.0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -1674,8 +1907,8 @@ int launch_update_f64(hipStream_t s, const CgState* st, int mode, int64_t n,
 
 __global__ void p_update_f64_kernel(const CgState* __restrict__ st, int64_t n,
                                     double* __restrict__ p, const double* __restrict__ r) {
-  if (st->done) return;
-  const double beta = st->beta;
+  if (ald(&st->done)) return;
+  const double beta = ald(&st->beta);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
     p[i] = -r[i] + beta * p[i];

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <stdint.h>
+#include <cstdlib>
 #include <string>
 
 namespace mr {
@@ -18,13 +19,24 @@ struct LaunchTiming {
   hipEvent_t stop = nullptr;
 };
 extern thread_local LaunchTiming t_launch;
+inline bool ext_launch_always() {   // debug: MR_EXT_LAUNCH=1
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MR_EXT_LAUNCH");
+    v = (e && atoi(e) == 1) ? 1 : 0;
+  }
+  return v == 1;
+}
 
 #define MR_LAUNCH(kernel, grid, block, shm, s, ...)                                  \
   do {                                                                               \
     hipEvent_t mr_ev0_ = ::mr::t_launch.start;                                       \
     ::mr::t_launch.start = nullptr;                                                  \
-    hipExtLaunchKernelGGL(kernel, grid, block, shm, s, mr_ev0_, ::mr::t_launch.stop, \
-                          0, __VA_ARGS__);                                           \
+    if (mr_ev0_ || ::mr::t_launch.stop || ::mr::ext_launch_always())                 \
+      hipExtLaunchKernelGGL(kernel, grid, block, shm, s, mr_ev0_, ::mr::t_launch.stop, \
+                            0, __VA_ARGS__);                                         \
+    else                                                                             \
+      hipLaunchKernelGGL(kernel, grid, block, shm, s, __VA_ARGS__);                  \
   } while (0)
 
 // Error handling --------------------------------------------------------------
