@@ -32,6 +32,7 @@ from movie_recommender_amd import synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_PEAK_TFS = 157.3        # MI355X FP32 vector / f32-MFMA dense peak
+GATHER_PEAK_GBS = 8600.0   # MI355X_MICROARCH.md: random rows, 38 MB table (Infinity Cache)
 METRIC = "ratings/sec per ALS iteration (MovieLens-full, k=64); RMSE parity"
 
 
@@ -224,14 +225,19 @@ def main():
     # snapshot (informational: the event timestamps of hipExtLaunchKernel
     # cost a few us per launch).
     plain_ms = None
+    replay_identical = None
     if not args.no_kernel_events:
         ctx.set_factors(*snap)
+        ctx.reset_stats()
         barrier()
         t1 = time.perf_counter()
         for s in range(args.steps):
             ctx.iterate(1)
         barrier()
         plain_ms = (time.perf_counter() - t1) * 1e3 / args.steps
+        st2 = ctx.stats()
+        replay_identical = (st2["cg_users_total"] == st["cg_users_total"]
+                            and st2["cg_items_total"] == st["cg_items_total"])
         if dist is not None:
             import torch
             tt = torch.tensor([plain_ms], dtype=torch.float64, device=f"cuda:{local_rank}")
@@ -261,6 +267,14 @@ def main():
         achieved, peak, unit = nbytes / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
     else:
         achieved, peak, unit = nflops / avg_s / 1e12, FP32_PEAK_TFS, "TFLOP/s"
+    # Gram kernels: the row gather (k floats of the other side's table per
+    # rating, Infinity-Cache resident) is the binding roofline; peak = the
+    # guide's measured random-row gather rate from a 38 MB table.
+    gather = None
+    if cls.startswith("gram"):
+        gb = n_local_users * 4.0 * k
+        gather = {"bytes_per_launch": int(gb), "achieved_GBps": round(gb / avg_s / 1e9, 1),
+                  "peak_GBps": GATHER_PEAK_GBS, "frac": round(gb / avg_s / 1e9 / GATHER_PEAK_GBS, 3)}
     traffic = None
     if os.path.exists(args.pmc):
         with open(args.pmc) as f:
@@ -297,7 +311,7 @@ def main():
                      "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
                      "traffic": traffic,
                      "alg_bytes_per_launch": int(nbytes), "alg_flops_per_launch": int(nflops),
-                     "avg_launch_us": round(avg_s * 1e6, 2)},
+                     "avg_launch_us": round(avg_s * 1e6, 2), "gather": gather},
         "cg_iterations": {"users_total": st["cg_users_total"],
                           "items_total": st["cg_items_total"],
                           "per_step_users": st["cg_users_total"] / args.steps,
@@ -305,6 +319,7 @@ def main():
         "kernels": kernel_table,
         "phase_ms_per_step": {p: round(v / args.steps, 3) for p, v in st["phase_ms"].items()},
         "ms_per_step_without_kernel_events": round(plain_ms, 3) if plain_ms else None,
+        "replay_cg_identical": replay_identical,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         try:

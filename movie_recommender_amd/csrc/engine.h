@@ -73,7 +73,6 @@ struct Engine {
   int chunk = 2048;
   bool fuse_start = true;   // CG start in the Gram epilogue (MR_FUSE_START=0: off)
   bool timing = false;
-  hipEvent_t hs_event = nullptr;   // half-step boundary marker (debug)
   std::vector<hipEvent_t> ev_pool;
   std::vector<Pending> pending;
   std::vector<PhaseSpan> spans;

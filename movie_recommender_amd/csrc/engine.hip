@@ -68,7 +68,6 @@ Engine::~Engine() {
     if (h_fac) (void)hipHostFree(h_fac);
     if (h_mirror) (void)hipHostFree(h_mirror);
     for (auto& e : ev_pool) (void)hipEventDestroy(e);
-    if (hs_event) (void)hipEventDestroy(hs_event);
     for (auto& p : pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto& sp : spans) if (sp.end) (void)hipEventDestroy(sp.end);
     if (rccl) (void)ncclCommDestroy((ncclComm_t)rccl);
@@ -164,8 +163,7 @@ int Engine::build_side(Side& S, bool user, int64_t n, const int32_t* d_key,
     return -1;
   // host copy of the offsets -> work list (chunks, heavy first)
   std::vector<int64_t> off(S.E + 1);
-  MR_HIP(hipMemcpyAsync(off.data(), S.off, (S.E + 1) * sizeof(int64_t),
-                        hipMemcpyDeviceToHost, stream));
+  MR_HIP(hipMemcpyAsync(off.data(), S.off, (S.E + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, stream));
   MR_HIP(hipStreamSynchronize(stream));
   std::vector<WorkItem> work;
   std::vector<SplitItem> split;
@@ -196,11 +194,9 @@ int Engine::build_side(Side& S, bool user, int64_t n, const int32_t* d_key,
       dalloc(&S.slab, S.n_slab * S.rec, stream))
     return -1;
   if (S.n_work)
-    MR_HIP(hipMemcpyAsync(S.work, work.data(), S.n_work * sizeof(WorkItem),
-                          hipMemcpyHostToDevice, stream));
+    MR_HIP(hipMemcpyAsync(S.work, work.data(), S.n_work * sizeof(WorkItem), hipMemcpyHostToDevice, stream));
   if (S.n_split)
-    MR_HIP(hipMemcpyAsync(S.split, split.data(), S.n_split * sizeof(SplitItem),
-                          hipMemcpyHostToDevice, stream));
+    MR_HIP(hipMemcpyAsync(S.split, split.data(), S.n_split * sizeof(SplitItem), hipMemcpyHostToDevice, stream));
   // normal equations + CG vectors
   const int64_t ef = S.E * ldk;
   if (dalloc(&S.G, S.E * gsize_of(k), stream) || dalloc(&S.C, ef, stream) ||
@@ -326,16 +322,7 @@ int Engine::init(int dev, int k_, int64_t U_, int64_t I_, int64_t n_u,
 // kernels read and write directly (zero-copy; fine-grained, system-coherent).
 // The earlier form -- a pageable hipMemcpyAsync into a pool buffer, then a
 // kernel -- let replays from one snapshot diverge run to run (a kernel saw
-// stale staging data).  MR_XFER_DMA=1 restores it for A/B checks.
-static bool xfer_dma() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("MR_XFER_DMA");
-    v = (e && atoi(e) == 1) ? 1 : 0;
-  }
-  return v == 1;
-}
-
+// stale staging data).
 int Engine::fac_stage(int64_t n) {
   if (n <= h_fac_n) return 0;
   if (h_fac) MR_HIP(hipHostFree(h_fac));
@@ -350,21 +337,6 @@ int Engine::set_factors(const double* hU, const double* hV) {
   MR_HIP(hipSetDevice(device));
   const int64_t nU = U * (k + 1), nV = I * (int64_t)k;
   int rc = 0;
-  if (xfer_dma()) {
-    double* tmp = nullptr;
-    if (dalloc(&tmp, nU + nV, stream)) return -1;
-    if (hU && U) {
-      MR_HIP(hipMemcpyAsync(tmp, hU, nU * 8, hipMemcpyHostToDevice, stream));
-      rc |= launch_unpack_factors(stream, U, k + 1, k, ldk, tmp, Ufac, Ubias);
-    }
-    if (hV && I) {
-      MR_HIP(hipMemcpyAsync(tmp + nU, hV, nV * 8, hipMemcpyHostToDevice, stream));
-      rc |= launch_unpack_factors(stream, I, k, k, ldk, tmp + nU, Vfac, nullptr);
-    }
-    MR_HIP(hipStreamSynchronize(stream));
-    dfree(tmp, stream);
-    return rc ? -1 : 0;
-  }
   MR_HIP(hipStreamSynchronize(stream));   // no kernel may still read h_fac
   if (fac_stage(nU + nV)) return -1;
   if (hU && U) {
@@ -383,23 +355,6 @@ int Engine::get_factors(double* hU, double* hV) {
   MR_HIP(hipSetDevice(device));
   const int64_t nU = U * (k + 1), nV = I * (int64_t)k;
   int rc = 0;
-  if (xfer_dma()) {
-    double* tmp = nullptr;
-    if (dalloc(&tmp, std::max(nU, nV), stream)) return -1;
-    if (hU && U) {
-      rc |= launch_pack_factors(stream, U, k + 1, k, ldk, Ufac, Ubias, tmp);
-      MR_HIP(hipMemcpyAsync(hU, tmp, nU * 8, hipMemcpyDeviceToHost, stream));
-      MR_HIP(hipStreamSynchronize(stream));
-    }
-    if (hV && I) {
-      rc |= launch_pack_factors(stream, I, k, k, ldk, Vfac, nullptr, tmp);
-      MR_HIP(hipMemcpyAsync(hV, tmp, nV * 8, hipMemcpyDeviceToHost, stream));
-      MR_HIP(hipStreamSynchronize(stream));
-    }
-    dfree(tmp, stream);
-    MR_HIP(hipStreamSynchronize(stream));
-    return rc ? -1 : 0;
-  }
   MR_HIP(hipStreamSynchronize(stream));
   if (fac_stage(nU + nV)) return -1;
   if (hU && U) rc |= launch_pack_factors(stream, U, k + 1, k, ldk, Ufac, Ubias, h_fac);
@@ -442,13 +397,11 @@ int Engine::allreduce_state_slot(int count) {
                           ncclSum, (ncclComm_t)rccl, stream));
     return 0;
   }
-  MR_HIP(hipMemcpyAsync(h_stage, &d_state->comm[0], count * sizeof(double),
-                        hipMemcpyDeviceToHost, stream));
+  MR_HIP(hipMemcpyAsync(h_stage, &d_state->comm[0], count * sizeof(double), hipMemcpyDeviceToHost, stream));
   MR_HIP(hipStreamSynchronize(stream));
   MR_CHECK(comm.allreduce_f64(comm.user, (double*)h_stage, count) == 0,
            "allreduce callback failed");
-  MR_HIP(hipMemcpyAsync(&d_state->comm[0], h_stage, count * sizeof(double),
-                        hipMemcpyHostToDevice, stream));
+  MR_HIP(hipMemcpyAsync(&d_state->comm[0], h_stage, count * sizeof(double), hipMemcpyHostToDevice, stream));
   return 0;
 }
 
@@ -478,8 +431,7 @@ int Engine::allgather_side(bool user) {
   const int64_t rowf = user ? ldk + 1 : ldk;
   std::vector<float> tab(rows * rowf);
   std::vector<float> fac(rows * ldk), bias(user ? rows : 0);
-  MR_HIP(hipMemcpyAsync(fac.data(), user ? Ufac : Vfac, rows * ldk * 4,
-                        hipMemcpyDeviceToHost, stream));
+  MR_HIP(hipMemcpyAsync(fac.data(), user ? Ufac : Vfac, rows * ldk * 4, hipMemcpyDeviceToHost, stream));
   if (user)
     MR_HIP(hipMemcpyAsync(bias.data(), Ubias, rows * 4, hipMemcpyDeviceToHost, stream));
   MR_HIP(hipStreamSynchronize(stream));
@@ -493,8 +445,7 @@ int Engine::allgather_side(bool user) {
     memcpy(&fac[r * ldk], &tab[r * rowf], ldk * 4);
     if (user) bias[r] = tab[r * rowf + ldk];
   }
-  MR_HIP(hipMemcpyAsync(user ? Ufac : Vfac, fac.data(), rows * ldk * 4,
-                        hipMemcpyHostToDevice, stream));
+  MR_HIP(hipMemcpyAsync(user ? Ufac : Vfac, fac.data(), rows * ldk * 4, hipMemcpyHostToDevice, stream));
   if (user)
     MR_HIP(hipMemcpyAsync(Ubias, bias.data(), rows * 4, hipMemcpyHostToDevice, stream));
   MR_HIP(hipStreamSynchronize(stream));
@@ -526,12 +477,7 @@ int Engine::wait_mirror(int target, CgMirror* out) {
       if (__atomic_load_n(&h_mirror->seq, __ATOMIC_ACQUIRE) == cur) return 0;
       continue;  // a newer state landed while copying: read again
     }
-    static int noq = -1;   // debug: MR_NO_QUERY=1 never queries the stream
-    if (noq < 0) {
-      const char* e = getenv("MR_NO_QUERY");
-      noq = (e && atoi(e) == 1) ? 1 : 0;
-    }
-    if (!noq && (++spins & 1023) == 0) {
+    if ((++spins & 1023) == 0) {
       const hipError_t q = hipStreamQuery(stream);
       if (q == hipSuccess) {
         if (__atomic_load_n(&h_mirror->seq, __ATOMIC_ACQUIRE) >= target) continue;
@@ -776,19 +722,6 @@ int Engine::half_step(bool user, double min_dec, int max_it, double* final_rr) {
     if (solve(S)) return -1;
   }
   if (allgather_side(user)) return -1;
-  {
-    static int hsm = -1;   // debug: MR_HS_MARKER = 1 marker event, 2 stream sync
-    if (hsm < 0) {
-      const char* e = getenv("MR_HS_MARKER");
-      hsm = e ? atoi(e) : 0;
-    }
-    if (hsm == 1) {
-      if (!hs_event) MR_HIP(hipEventCreate(&hs_event));
-      MR_HIP(hipEventRecord(hs_event, stream));
-    } else if (hsm == 2) {
-      MR_HIP(hipStreamSynchronize(stream));
-    }
-  }
   if (timing) {
     hipEvent_t end = nullptr;
     if (sharded()) {   // the RCCL exchange belongs to the solve phase
@@ -874,8 +807,7 @@ int Engine::get_normal_equations(bool user, int n, const int* ents, double* G, d
   for (int t = 0; t < n; ++t) {
     const int64_t e = ents[t];
     MR_CHECK(e >= 0 && e < S.E, "entity out of range");
-    MR_HIP(hipMemcpyAsync(g.data(), S.G + e * gsize_of(k), gsize_of(k) * 4,
-                          hipMemcpyDeviceToHost, stream));
+    MR_HIP(hipMemcpyAsync(g.data(), S.G + e * gsize_of(k), gsize_of(k) * 4, hipMemcpyDeviceToHost, stream));
     MR_HIP(hipMemcpyAsync(v.data(), S.C + e * ldk, ldk * 4, hipMemcpyDeviceToHost, stream));
     if (user) {
       MR_HIP(hipMemcpyAsync(s.data(), S.Gs + e * ldk, ldk * 4, hipMemcpyDeviceToHost, stream));

@@ -1047,15 +1047,12 @@ static int launch_gram_g(hipStream_t s, bool user_side, int k, const WorkItem* w
 // on MI355X (tools/ab_variants.sh, ML-full shape, k = 64): G = 2 with 4
 // buffers is best (Gram 926 / 830 us vs 959 / 858 with G = 4, 2 buffers);
 // MR_GRAM_G=2|4|8 overrides (tuning).
+// Read per launch (a getenv), so tests can switch paths inside one process.
 static int gram_group_size(int nb) {
-  static int env = -2;
-  if (env == -2) {
-    const char* e = getenv("MR_GRAM_G");
-    const char* b = getenv("MR_GRAM_BF3");
-    env = (b && atoi(b) == 0) ? (e ? atoi(e) : 2) : 0;
-  }
-  if (env == 0 || env == 2 || env == 4) return env;
-  return 2;
+  const char* e = getenv("MR_GRAM_G");
+  const char* b = getenv("MR_GRAM_BF3");
+  const int g = (b && atoi(b) == 0) ? (e ? atoi(e) : 2) : 0;
+  return (g == 0 || g == 2 || g == 4) ? g : 2;
 }
 
 template <int NB>

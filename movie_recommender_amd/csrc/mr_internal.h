@@ -19,20 +19,13 @@ struct LaunchTiming {
   hipEvent_t stop = nullptr;
 };
 extern thread_local LaunchTiming t_launch;
-inline bool ext_launch_always() {   // debug: MR_EXT_LAUNCH=1
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("MR_EXT_LAUNCH");
-    v = (e && atoi(e) == 1) ? 1 : 0;
-  }
-  return v == 1;
-}
 
+// Untimed launches (no slot events) take the plain launch path.
 #define MR_LAUNCH(kernel, grid, block, shm, s, ...)                                  \
   do {                                                                               \
     hipEvent_t mr_ev0_ = ::mr::t_launch.start;                                       \
     ::mr::t_launch.start = nullptr;                                                  \
-    if (mr_ev0_ || ::mr::t_launch.stop || ::mr::ext_launch_always())                 \
+    if (mr_ev0_ || ::mr::t_launch.stop)                                              \
       hipExtLaunchKernelGGL(kernel, grid, block, shm, s, mr_ev0_, ::mr::t_launch.stop, \
                             0, __VA_ARGS__);                                         \
     else                                                                             \

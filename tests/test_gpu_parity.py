@@ -128,13 +128,53 @@ def test_engine_matches_abi_and_is_deterministic(gpu):
     assert np.array_equal(U2, U3) and np.array_equal(V2, V3)   # bitwise reproducible
 
 
-@pytest.mark.parametrize("k,gram3", [(3, 0), (10, 0), (16, 0), (32, 0), (33, 0), (64, 0),
-                                     (65, 0), (96, 0), (128, 0), (20, 1), (32, 1), (64, 1)])
-def test_gram_kernel_vs_numpy(gpu, k, gram3, monkeypatch):
+def test_replay_from_snapshot_is_bitwise_identical(gpu):
+    """A set -> get factor round trip is exact and replays of the same steps
+    from one snapshot are bitwise identical, with and without per-launch
+    timing events (bench.py's event-free pass relies on this).  Regression:
+    pageable DMA staging once returned stale factor data (xfer.hip)."""
+    from movie_recommender_amd import synth
+    from movie_recommender_amd.engine import AlsContext
+    k = 64
+    rs = synth.movielens_like("ml-full", k, scale=0.02)
+    rng = np.random.RandomState(0)
+    U0 = rng.uniform(-1, 1, rs.num_users * (k + 1))
+    V0 = rng.uniform(-1, 1, rs.num_items * k)
+    with AlsContext(rs.user_ids, rs.item_ids, rs.ratings, k, rs.num_users,
+                    rs.num_items) as ctx:
+        ctx.set_factors(U0, V0)
+        ctx.iterate(2)
+        snap = tuple(a.copy() for a in ctx.get_factors())
+        for _ in range(3):
+            ctx.set_factors(*snap)
+            U, V = ctx.get_factors()
+            assert np.array_equal(U, snap[0]) and np.array_equal(V, snap[1])
+        outs = []
+        for timing in (True, False, True, False):
+            ctx.set_factors(*snap)
+            ctx.reset_stats()
+            ctx.set_timing(timing)
+            ctx.iterate(3)
+            st = ctx.stats()
+            outs.append((ctx.get_factors(), st["cg_users_total"], st["cg_items_total"]))
+        ctx.set_timing(False)
+    (U1, V1), cu, ci = outs[0]
+    for (U, V), cu2, ci2 in outs[1:]:
+        assert (cu2, ci2) == (cu, ci)
+        assert np.array_equal(U, U1) and np.array_equal(V, V1)
+
+
+@pytest.mark.parametrize("k,path", [(3, "bf3"), (10, "bf3"), (16, "bf3"), (32, "bf3"),
+                                    (33, "bf3"), (64, "bf3"), (65, "bf3"), (96, "bf3"),
+                                    (128, "bf3"), (10, "f32"), (33, "f32"), (64, "f32"),
+                                    (128, "f32"), (20, "gram3"), (64, "gram3")])
+def test_gram_kernel_vs_numpy(gpu, k, path, monkeypatch):
     """Normal equations of both sides against fp64 NumPy, including heavy
-    entities split across waves (chunk 64 forces slabs) and empty entities;
-    gram3 = 1 runs the bf16x3 matrix-core kernel (MR_GRAM3=1)."""
-    monkeypatch.setenv("MR_GRAM3", str(gram3))
+    entities split across waves (chunk 64 forces slabs) and empty entities.
+    Paths: bf3 = default in-register bf16x3 split on the bf16 MFMA; f32 = the
+    fp32 MFMA loop (MR_GRAM_BF3=0); gram3 = pre-split table (MR_GRAM3=1)."""
+    monkeypatch.setenv("MR_GRAM3", "1" if path == "gram3" else "0")
+    monkeypatch.setenv("MR_GRAM_BF3", "0" if path == "f32" else "1")
     from movie_recommender_amd.engine import AlsContext
     from oracle import als_oracle as O
     rng = np.random.default_rng(k)
