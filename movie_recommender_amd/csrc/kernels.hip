@@ -1182,19 +1182,18 @@ int launch_slab_reduce(hipStream_t s, bool user_side, int k,
 // product T^T v_bi into y_bj; the 4-lane row partials and 16-lane column
 // partials are combined once per entity through LDS in a fixed order.
 // ---------------------------------------------------------------------------
-// The CG state is shared by every block of consecutive kernels running on
-// all 8 XCDs, whose L2s are not coherent with each other: every kernel reads
-// it with agent-scope (sc1) loads and the single finalizing thread writes it
-// with agent-scope stores, so no block ever sees a line its XCD's L2 cached
-// before the previous kernel updated it.  (Plain accesses made replays of the
-// same steps diverge depending on launch timing.)
+// CG state access.  The state passes between kernels like every other buffer
+// (kernel boundaries order it), so plain loads / stores suffice.  Agent-scope
+// atomics here cost ~60 us per GEMV launch (the finalizing block's ~30
+// dependent round trips) and were not needed: the replay divergence they were
+// meant to fix came from the factor snapshot transfers.
 template <class T>
 __device__ __forceinline__ T ald(const T* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return *p;
 }
 template <class T>
 __device__ __forceinline__ void ast(T* p, T v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  *p = v;
 }
 
 struct CgScalars {   // the fields the rules read and write
