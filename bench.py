@@ -55,7 +55,7 @@ def load_data(shape, k, cache_dir="/tmp"):
     return rs
 
 
-def algorithmic_cost(cls, k, n_users, n_items, n_ratings, ldk):
+def algorithmic_cost(cls, k, n_users, n_items, n_ratings, ldk, fused=True):
     """(bytes, flops) per launch of a kernel class; definitions in DESIGN.md.
 
     Normal equations are stored "tri16" (mr_internal.h): the nb(nb-1)/2
@@ -68,70 +68,65 @@ def algorithmic_cost(cls, k, n_users, n_items, n_ratings, ldk):
     minimum work; SURVEY.md 8(d)'s F(k) counts the full K x K product, which
     would put a symmetric kernel above the MFMA peak.  The kernel's executed
     MFMA work is nb(nb+1)/2 * 512 flop per rating (diagonal blocks full).
-    With the fused CG start (default) the Gram launch also writes r, p, q."""
+    With the fused CG start (default) the Gram launch also reads x and writes
+    r, p, q.  CG vectors r / p / q are fp64 (8 B), x and G fp32 (4 B)."""
     K = k + 1
     nb = (k + 15) // 16
     gsz = (nb * (nb - 1) // 2 + nb // 2 + nb % 2) * 256 + (nb // 2) * 16
     if cls == "matvec_users":
         E = n_users
         g = E * (gsz + ldk + 1) * 4               # G_e blocks + Gs row + count
-        v = E * (ldk + 1) * 4 * 4                 # p read+write, r read, Ap write
+        v = E * (ldk + 1) * 8 * 4                 # p read+write, r read, Ap write (fp64)
         return g + v, E * 2.0 * K * K
     if cls == "matvec_items":
         E = n_items
-        return E * gsz * 4 + E * ldk * 4 * 4, E * 2.0 * k * k
-    fused = os.environ.get("MR_FUSE_START", "1") != "0"
+        return E * gsz * 4 + E * ldk * 8 * 4, E * 2.0 * k * k
     if cls == "gram_users":
         # per rating: (idx, value) 8 B + gathered item row k*4 B; output blocks
         b = n_ratings * (8 + 4 * k) + n_users * (gsz + 2 * ldk + 2) * 4
-        if fused:   # x read, r / p / q written
-            b += n_users * (ldk + 1) * 4 * 4
+        if fused:   # x read (fp32), r / p / q written (fp64)
+            b += n_users * (ldk + 1) * (4 + 3 * 8)
         return b, n_ratings * (1.0 * K * (K + 1) + 2.0 * K)
     if cls == "gram_items":
         b = n_ratings * (8 + 4 * (k + 1)) + n_items * (gsz + ldk) * 4
         if fused:
-            b += n_items * ldk * 4 * 4
+            b += n_items * ldk * (4 + 3 * 8)
         return b, n_ratings * (1.0 * k * (k + 1) + 2.0 * k)
     if cls == "cg_update":
+        # x rw (fp32), r rw, p read, q read (fp64)
         E = (n_users * (ldk + 1) + n_items * ldk) / 2.0   # average side
-        return E * 6 * 4, E * 4.0
+        return E * (2 * 4 + 4 * 8), E * 4.0
     return 0, 0
 
 
-def cpu_baseline(rs, k, threads, frac, seed=0):
-    """Reference CPU path on a bounded sample: a random fraction of users with
-    all their ratings (ids compacted), t_iter = (T(3) - T(1)) / 2 as in
-    BASELINE.md.  Returns a dict for the JSON line, or None if unavailable."""
+def cpu_baseline(shape, k, threads, scale, seed=0):
+    """Reference CPU path on a bounded sample of the same workload: the
+    MovieLens-shaped generator at ``scale`` of the users, items and draws (so
+    per-entity degrees, and with them the CPU's per-rating costs, keep their
+    full-size distribution; a user subsample would keep every item and with
+    it the reference's full-length per-thread SpMV^T scratch), shrunk for the
+    same k.  t_iter = (T(3) - T(1)) / 2 as in BASELINE.md.  Returns a dict for
+    the JSON line, or None if the reference build is unavailable."""
     from oracle import ref
     if not ref.available():
         return None
-    rng = np.random.default_rng(seed)
-    keep_users = rng.random(rs.num_users) < frac
-    sel = keep_users[rs.user_ids]
-    u = rs.user_ids[sel]
-    i = rs.item_ids[sel]
-    r = rs.ratings[sel]
-    _, u = np.unique(u, return_inverse=True)
-    _, i = np.unique(i, return_inverse=True)
-    u = u.astype(np.int32)
-    i = i.astype(np.int32)
-    nu, ni = int(u.max()) + 1, int(i.max()) + 1
-    U0, V0 = ref.init_factors(nu, ni, k, 0)
+    rs = synth.movielens_like(shape, k, scale=scale)
+    U0, V0 = ref.init_factors(rs.num_users, rs.num_items, k, seed)
     ref.set_thread_count(threads)
     t = {}
-    its = {}
     for n_it in (1, 3):
         t0 = time.perf_counter()
-        _, _, ret = ref.als(u, i, r, k, U0, V0, max_iteration=n_it)
+        ref.als(rs.user_ids, rs.item_ids, rs.ratings, k, U0, V0, max_iteration=n_it)
         t[n_it] = time.perf_counter() - t0
-        its[n_it] = ret
     t_iter = (t[3] - t[1]) / 2.0
-    return {"value": len(r) / t_iter, "unit": "ratings/s", "cores": threads,
+    return {"value": rs.n / t_iter, "unit": "ratings/s", "cores": threads,
+            "host_cpus": os.cpu_count(),
             "kind": "reference",
-            "sample": (f"{frac:.3f} of users of the same workload with all their ratings: "
-                       f"N={len(r)}, users={nu}, items={ni}, k={k}; t_iter=(T(3)-T(1))/2 = "
-                       f"{t_iter:.3f} s (T1={t[1]:.2f} s, T3={t[3]:.2f} s); "
-                       f"oracle/_ref/cpp_ls_lib.so built from /root/reference/cpp/ls_lib -O2")}
+            "sample": (f"{shape} generator at scale {scale} (users, items, draws), shrunk for "
+                       f"k={k}: N={rs.n}, users={rs.num_users}, items={rs.num_items}; "
+                       f"t_iter=(T(3)-T(1))/2 = {t_iter:.3f} s (T1={t[1]:.2f} s, "
+                       f"T3={t[3]:.2f} s); oracle/_ref/cpp_ls_lib.so built from "
+                       f"/root/reference/cpp/ls_lib -O2, {threads} threads")}
 
 
 def main():
@@ -146,7 +141,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="time steps without per-launch HIP events (no roofline)")
-    ap.add_argument("--cpu-frac", type=float, default=0.08)
+    ap.add_argument("--cpu-scale", type=float, default=0.25)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--force-shard", action="store_true",
                     help="use the sharded RCCL path even with one rank (testing)")
@@ -251,7 +246,7 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
 
     # dominant kernel and its roofline (rank 0's kernels)
-    ldk = (k + 3) // 4 * 4
+    ldk = (k + 15) // 16 * 16
     if args.no_kernel_events:
         st["kernel_ms"] = {"none": 1.0}
         st["kernel_launches"] = {"none": 1}
@@ -323,7 +318,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
-            cb = cpu_baseline(rs, k, args.cpu_threads, args.cpu_frac)
+            cb = cpu_baseline(args.shape, k, args.cpu_threads, args.cpu_scale)
         except Exception as e:  # the GPU number stands on its own
             log(f"[bench] cpu baseline failed: {e!r}")
             cb = None

@@ -119,6 +119,18 @@ int mr_als_get_factors(mr_als* ctx, double* U, double* V);
 int mr_als_set_solver(mr_als* ctx, int solver, double ridge);
 /* Timing of every kernel launch with HIP events (off by default). */
 int mr_als_set_timing(mr_als* ctx, int enable);
+/* Engine options (mr_als_set_option):
+ *   MR_OPT_FUSE_START     1 (default): the Gram kernel also starts the CG solve
+ *                         (r0, p0, q0 = G p0 from its accumulators); 0: the
+ *                         reference's order, one matvec + update pass
+ *   MR_OPT_CG_SPECULATE   1 (default): enqueue CG iteration t+1 before t's
+ *                         state is read back when t provably cannot stop
+ *                         (ignored in sharded runs); 0: one iteration ahead
+ *   MR_OPT_WAIT_TIMEOUT_S host wait for a published CG state, seconds
+ *                         (default 300; a stalled peer rank then fails the
+ *                         call instead of hanging it) */
+enum { MR_OPT_FUSE_START = 0, MR_OPT_CG_SPECULATE = 1, MR_OPT_WAIT_TIMEOUT_S = 2 };
+int mr_als_set_option(mr_als* ctx, int option, double value);
 /* Ratings per Gram work item: heavier entities are split across waves and
  * their partial normal equations combined in order.  Applies to contexts
  * created afterwards (default 2048). */
@@ -133,6 +145,11 @@ int mr_als_iterate(mr_als* ctx, int n);
  * iteration count (CG mode) or 0; *final_rr may be NULL. */
 int mr_als_half_step(mr_als* ctx, int side, double* final_rr);
 
+/* The same with the CG arguments of cg_least_squares (matrix.cpp:456):
+ * min_r_decrease and max_iteration (max_iteration 0: only r0, rr = r0.r0). */
+int mr_als_half_step_ex(mr_als* ctx, int side, double min_r_decrease, int max_iteration,
+                        double* final_rr);
+
 /* Build (only) the normal equations of one side from the current factors. */
 int mr_als_build_normal_equations(mr_als* ctx, int side);
 /* Copy the normal equations of n local entities of `side` (as last built):
@@ -140,6 +157,10 @@ int mr_als_build_normal_equations(mr_als* ctx, int side);
  * items.  For checking the Gram kernel at any problem size. */
 int mr_als_get_normal_equations(mr_als* ctx, int side, int n, const int* entities,
                                 double* G_out, double* c_out);
+
+/* The CG vectors r, p, q (fp64, E*K each; K = k+1 per user with the bias
+ * entry last, k per item) of the side's last solve; any may be NULL.  Tests. */
+int mr_als_get_cg_vectors(mr_als* ctx, int side, double* r, double* p, double* q);
 
 int mr_als_get_stats(mr_als* ctx, mr_stats* out);
 int mr_als_reset_stats(mr_als* ctx);

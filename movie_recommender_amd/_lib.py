@@ -100,10 +100,13 @@ SIGNATURES = {
     "mr_als_get_factors": (ctypes.c_int, [VP, DP, DP]),
     "mr_als_set_solver": (ctypes.c_int, [VP, ctypes.c_int, ctypes.c_double]),
     "mr_als_set_timing": (ctypes.c_int, [VP, ctypes.c_int]),
+    "mr_als_set_option": (ctypes.c_int, [VP, ctypes.c_int, ctypes.c_double]),
     "mr_set_gram_chunk": (ctypes.c_int, [ctypes.c_int]),
     "mr_als_run": (ctypes.c_int, [VP, ctypes.c_double, ctypes.c_int]),
     "mr_als_iterate": (ctypes.c_int, [VP, ctypes.c_int]),
     "mr_als_half_step": (ctypes.c_int, [VP, ctypes.c_int, DP]),
+    "mr_als_get_cg_vectors": (ctypes.c_int, [VP, ctypes.c_int, DP, DP, DP]),
+    "mr_als_half_step_ex": (ctypes.c_int, [VP, ctypes.c_int, ctypes.c_double, ctypes.c_int, DP]),
     "mr_als_build_normal_equations": (ctypes.c_int, [VP, ctypes.c_int]),
     "mr_als_get_normal_equations": (ctypes.c_int, [VP, ctypes.c_int, ctypes.c_int, IP, DP, DP]),
     "mr_als_get_stats": (ctypes.c_int, [VP, ctypes.POINTER(MrStats)]),

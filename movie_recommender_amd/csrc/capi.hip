@@ -222,6 +222,19 @@ int mr_als_set_timing(mr_als* ctx, int enable) {
   return 0;
 }
 
+int mr_als_set_option(mr_als* ctx, int option, double value) {
+  MR_CHECK(ctx, "null context");
+  switch (option) {
+    case MR_OPT_FUSE_START: ctx->eng.fuse_start = value != 0.0; return 0;
+    case MR_OPT_CG_SPECULATE: ctx->eng.speculate = value != 0.0; return 0;
+    case MR_OPT_WAIT_TIMEOUT_S:
+      MR_CHECK(value > 0.0, "timeout must be > 0");
+      ctx->eng.wait_timeout_s = value;
+      return 0;
+    default: MR_CHECK(false, "unknown option");
+  }
+}
+
 int mr_set_gram_chunk(int chunk) {
   MR_CHECK(chunk >= 64 && chunk <= (1 << 30), "chunk must be in [64, 2^30]");
   g_gram_chunk = chunk;
@@ -245,6 +258,16 @@ int mr_als_half_step(mr_als* ctx, int side, double* final_rr) {
       [&]() { return ctx->eng.half_step(side == MR_SIDE_USERS, 0.01, 200, final_rr); });
 }
 
+int mr_als_half_step_ex(mr_als* ctx, int side, double min_r_decrease, int max_iteration,
+                        double* final_rr) {
+  MR_CHECK(ctx, "null context");
+  MR_CHECK(side == MR_SIDE_USERS || side == MR_SIDE_ITEMS, "unknown side");
+  MR_CHECK(max_iteration >= 0, "max_iteration must be >= 0");
+  return guarded([&]() {
+    return ctx->eng.half_step(side == MR_SIDE_USERS, min_r_decrease, max_iteration, final_rr);
+  });
+}
+
 int mr_als_build_normal_equations(mr_als* ctx, int side) {
   MR_CHECK(ctx, "null context");
   MR_CHECK(side == MR_SIDE_USERS || side == MR_SIDE_ITEMS, "unknown side");
@@ -255,6 +278,12 @@ int mr_als_build_normal_equations(mr_als* ctx, int side) {
     MR_HIP(hipStreamSynchronize(ctx->eng.stream));
     return 0;
   });
+}
+
+int mr_als_get_cg_vectors(mr_als* ctx, int side, double* r, double* p, double* q) {
+  MR_CHECK(ctx, "null context");
+  MR_CHECK(side == MR_SIDE_USERS || side == MR_SIDE_ITEMS, "unknown side");
+  return guarded([&]() { return ctx->eng.get_cg_vectors(side == MR_SIDE_USERS, r, p, q); });
 }
 
 int mr_als_get_normal_equations(mr_als* ctx, int side, int n, const int* entities,

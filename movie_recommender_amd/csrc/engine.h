@@ -26,8 +26,8 @@ struct Side {
   float* slab = nullptr;
   int64_t n_slab = 0, rec = 0;
   float *G = nullptr, *Gs = nullptr, *Gn = nullptr, *C = nullptr, *Cb = nullptr;
-  float *r = nullptr, *p = nullptr, *q = nullptr;
-  float *rb = nullptr, *pb = nullptr, *qb = nullptr;
+  double *r = nullptr, *p = nullptr, *q = nullptr;     // fp64 CG vectors [E][ldk]
+  double *rb = nullptr, *pb = nullptr, *qb = nullptr;  // user side: bias entries [E]
   int n_part_mv = 1;
   double* start_parts = nullptr;   // fused CG start: (r.r, p.Gp) per block
   int64_t n_start_pairs = 0;
@@ -53,8 +53,6 @@ struct Engine {
   int k = 0, ldk = 0;
   int64_t U = 0, I = 0, N = 0;
   float *Ufac = nullptr, *Ubias = nullptr, *Vfac = nullptr;
-  uint16_t* Fsplit = nullptr;   // bf16x3 copy of the gathered table (gram3)
-  bool use_gram3 = false;
   Side su, si;
   CgState* d_state = nullptr;
   CgState* h_state = nullptr;
@@ -71,7 +69,12 @@ struct Engine {
   int solver = MR_SOLVER_CG;
   double ridge = 0.0;
   int chunk = 2048;
-  bool fuse_start = true;   // CG start in the Gram epilogue (MR_FUSE_START=0: off)
+  bool fuse_start = true;   // CG start in the Gram epilogue (MR_OPT_FUSE_START)
+  bool speculate = true;    // enqueue CG iteration t+1 before t's state is known
+                            // when t provably cannot stop (MR_OPT_CG_SPECULATE;
+                            // never in sharded runs: every rank must issue the
+                            // same collectives)
+  double wait_timeout_s = 300.0;   // host wait for a published CG state
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
   std::vector<Pending> pending;
@@ -114,6 +117,7 @@ struct Engine {
   int iterate(int n);
   int predict(int64_t n, const int* uid, const int* iid, double* out);
   int get_normal_equations(bool user, int n, const int* ents, double* G, double* c);
+  int get_cg_vectors(bool user, double* r, double* p, double* q);
   // timing
   int ev_get(hipEvent_t* e);
   int tic(int cls, int tag, hipEvent_t* a);

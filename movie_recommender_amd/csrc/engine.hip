@@ -8,6 +8,7 @@
 // but every numeric step runs on the GPU; the host only enqueues kernels and
 // reads the 72-byte CG state once per chunk of CG iterations.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -59,7 +60,7 @@ Engine::~Engine() {
     (void)hipStreamSynchronize(stream);
     free_side(su, stream);
     free_side(si, stream);
-    dfree(Ufac, stream); dfree(Ubias, stream); dfree(Vfac, stream); dfree(Fsplit, stream);
+    dfree(Ufac, stream); dfree(Ubias, stream); dfree(Vfac, stream);
     dfree(d_state, stream); dfree(partials, stream); dfree(d_flag, stream);
     (void)hipStreamSynchronize(stream);
     if (h_state) (void)hipHostFree(h_state);
@@ -202,15 +203,21 @@ int Engine::build_side(Side& S, bool user, int64_t n, const int32_t* d_key,
   if (dalloc(&S.G, S.E * gsize_of(k), stream) || dalloc(&S.C, ef, stream) ||
       dalloc(&S.r, ef, stream) || dalloc(&S.p, ef, stream) || dalloc(&S.q, ef, stream))
     return -1;
+  // padding columns (n >= k) of the CG vectors stay exactly zero
   if (user) {
     if (dalloc(&S.Gs, ef, stream) || dalloc(&S.Gn, S.E, stream) ||
         dalloc(&S.Cb, S.E, stream) || dalloc(&S.rb, S.E, stream) ||
         dalloc(&S.pb, S.E, stream) || dalloc(&S.qb, S.E, stream))
       return -1;
   }
-  MR_HIP(hipMemsetAsync(S.r, 0, ef * sizeof(float), stream));
-  MR_HIP(hipMemsetAsync(S.p, 0, ef * sizeof(float), stream));
-  MR_HIP(hipMemsetAsync(S.q, 0, ef * sizeof(float), stream));
+  MR_HIP(hipMemsetAsync(S.r, 0, ef * sizeof(double), stream));
+  MR_HIP(hipMemsetAsync(S.p, 0, ef * sizeof(double), stream));
+  MR_HIP(hipMemsetAsync(S.q, 0, ef * sizeof(double), stream));
+  if (user) {
+    MR_HIP(hipMemsetAsync(S.rb, 0, S.E * sizeof(double), stream));
+    MR_HIP(hipMemsetAsync(S.pb, 0, S.E * sizeof(double), stream));
+    MR_HIP(hipMemsetAsync(S.qb, 0, S.E * sizeof(double), stream));
+  }
   // fused CG start: one (r.r, p.Gp) pair per Gram block, then per split block
   S.n_start_pairs = gram_blocks(S.n_work) + (S.n_split + 3) / 4;
   if (dalloc(&S.start_parts, 2 * std::max<int64_t>(1, S.n_start_pairs), stream)) return -1;
@@ -257,17 +264,6 @@ int Engine::init(int dev, int k_, int64_t U_, int64_t I_, int64_t n_u,
   MR_HIP(hipMemsetAsync(Ufac, 0, (U + 1) * ldk * 4, stream));
   MR_HIP(hipMemsetAsync(Ubias, 0, (U + 1) * 4, stream));
   MR_HIP(hipMemsetAsync(Vfac, 0, (I + 1) * ldk * 4, stream));
-  // bf16x3 matrix-core normal equations (gram3.hip) on request (MR_GRAM3=1):
-  // parity-green, but at k = 64 it measures level with the f32 MFMA kernel
-  // (0.96 / 0.89-1.17 ms vs 0.92-1.0 ms per side), so the f32 kernel stays the
-  // default (DESIGN.md "Gram kernel variants")
-  {
-    const char* e = getenv("MR_GRAM3");
-    use_gram3 = gram3_supported(k) && e && atoi(e) == 1;
-    const char* f = getenv("MR_FUSE_START");
-    fuse_start = !(f && atoi(f) == 0);
-  }
-  if (use_gram3 && dalloc(&Fsplit, (std::max(U, I) + 1) * 3 * ldk, stream)) return -1;
   // upload + build both views
   const bool same = (uv_uid == iv_uid && uv_iid == iv_iid && uv_r == iv_r && n_u == n_i);
   for (int view = 0; view < (same ? 1 : 2); ++view) {
@@ -464,27 +460,41 @@ int Engine::finalize_sharded(int phase, int seq) {
 }
 
 // Spin on the host-mapped mirror until a state with seq >= target has been
-// published.  Checks the stream for errors, and for "stream idle but nothing
-// published" (which would be a bug) instead of hanging.
+// published.  Seqlock protocol (publish(), kernels.hip): the device stores
+// 2 seq - 1 (odd: write in progress), the fields, then 2 seq (release); a
+// copy is accepted only if it was bracketed by the same even value.  Checks
+// the stream for errors and for "stream idle but nothing published" (a bug),
+// and gives up after wait_timeout_s (a stalled peer rank in a sharded run).
 int Engine::wait_mirror(int target, CgMirror* out) {
+  const int want = 2 * target;
   long spins = 0;
+  const auto t0 = std::chrono::steady_clock::now();
   while (true) {
-    const int cur = __atomic_load_n(&h_mirror->seq, __ATOMIC_ACQUIRE);
-    if (cur >= target) {
-      *out = *h_mirror;
-      out->seq = cur;
+    const int s1 = __atomic_load_n(&h_mirror->seq, __ATOMIC_ACQUIRE);
+    if (!(s1 & 1) && s1 >= want) {
+      CgMirror m;
+      memcpy(&m, (const void*)h_mirror, sizeof(CgMirror));
       __atomic_thread_fence(__ATOMIC_ACQUIRE);
-      if (__atomic_load_n(&h_mirror->seq, __ATOMIC_ACQUIRE) == cur) return 0;
+      if (__atomic_load_n(&h_mirror->seq, __ATOMIC_ACQUIRE) == s1) {
+        *out = m;
+        out->seq = s1 / 2;
+        return 0;
+      }
       continue;  // a newer state landed while copying: read again
     }
     if ((++spins & 1023) == 0) {
       const hipError_t q = hipStreamQuery(stream);
       if (q == hipSuccess) {
-        if (__atomic_load_n(&h_mirror->seq, __ATOMIC_ACQUIRE) >= target) continue;
+        const int s2 = __atomic_load_n(&h_mirror->seq, __ATOMIC_ACQUIRE);
+        if (!(s2 & 1) && s2 >= want) continue;
         MR_CHECK(false, "CG state was not published (stream idle)");
       }
       MR_CHECK(q == hipErrorNotReady,
                std::string("stream error while polling CG state: ") + hipGetErrorString(q));
+      const double el =
+          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      MR_CHECK(el < wait_timeout_s, "timed out waiting for the CG state (" +
+                                        std::to_string(el) + " s; stalled peer rank?)");
     }
     __builtin_ia32_pause();
   }
@@ -530,17 +540,10 @@ int Engine::gram(Side& S, bool start) {
   const int cls = user ? MR_K_GRAM_USERS : MR_K_GRAM_ITEMS;
   if (tic(cls, -1, &a)) return -1;
   const int zrow = (int)(user ? I : U);
-  if (use_gram3) {
-    if (launch_split_table(stream, zrow + 1, k, F, Fsplit) ||
-        launch_gram3(stream, user, k, S.work, S.n_work, S.idx, S.val, Fsplit, bias, zrow,
-                     direct_dst(S), slab_dst(S)))
-      return -1;
-  } else {
-    const CgStart cs = cg_start_of(S);
-    if (launch_gram(stream, user, k, S.work, S.n_work, S.idx, S.val, F, bias, zrow,
-                    direct_dst(S), slab_dst(S), start ? &cs : nullptr))
-      return -1;
-  }
+  const CgStart cs = cg_start_of(S);
+  if (launch_gram(stream, user, k, S.work, S.n_work, S.idx, S.val, F, bias, zrow,
+                  direct_dst(S), slab_dst(S), start ? &cs : nullptr))
+    return -1;
   if (toc(cls, -1, a)) return -1;
   if (S.n_split) {
     if (tic(MR_K_SLAB_REDUCE, -1, &a)) return -1;
@@ -617,9 +620,11 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr, bool start
     if (toc(MR_K_CG_CONTROL, -1, a)) return -1;
   } else {
     MR_HIP(hipMemcpyAsync(d_state, h_init, sizeof(CgState), hipMemcpyHostToDevice, stream));
-    // r0 = G x - c ; p0 = -r0 ; rr  (matrix.cpp:464-485)
+    // r0 = G x - c ; p0 = -r0 ; rr  (matrix.cpp:464-485): p holds x in fp64
+    // for the matvec, which forms q = G x; the INIT update overwrites p
+    if (launch_x_to_vec(stream, n, nb, xf, xb, S.p, S.pb)) return -1;
     if (tic(mv_cls, -1, &a)) return -1;
-    if (launch_cg_matvec(stream, user, d_state, 0, S.E, k, S.G, S.Gs, S.Gn, xf, xb,
+    if (launch_cg_matvec(stream, user, d_state, 0, S.E, k, S.G, S.Gs, S.Gn, S.p, S.pb,
                          S.r, S.rb, S.q, S.qb, partials, S.n_part_mv))
       return -1;
     if (toc(mv_cls, -1, a)) return -1;
@@ -658,11 +663,11 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr, bool start
   // only after two stagnating steps, so both are enqueued behind the init
   // without waiting for its state (they are no-ops if the init already
   // finished the solve: rr < 1e-6 or max_it == 0).
-  static int spec = -1;     // MR_CG_SPEC=0: no speculative launches (debug)
-  if (spec < 0) {
-    const char* e = getenv("MR_CG_SPEC");
-    spec = (e && atoi(e) == 0) ? 0 : 1;
-  }
+  // Sharded runs never speculate: a rank's launch count would then depend on
+  // its host's timing, and every launched iteration issues collectives that
+  // must match across ranks.  With one outstanding iteration the launch
+  // sequence is the same on every rank.
+  const int spec = (speculate && !shard) ? 1 : 0;
   int launched = 0;          // iterations enqueued so far
   for (; launched < std::min(spec ? 2 : 1, max_it); ++launched)
     if (launch_iter(launched)) return -1;
@@ -710,7 +715,7 @@ int Engine::half_step(bool user, double min_dec, int max_it, double* final_rr) {
   MR_HIP(hipSetDevice(device));
   Side& S = user ? su : si;
   const size_t g0 = pending.size();
-  const bool fused = solver == MR_SOLVER_CG && fuse_start && !use_gram3;
+  const bool fused = solver == MR_SOLVER_CG && fuse_start;
   if (gram(S, fused)) return -1;
   const size_t c0 = pending.size();
   int its = 0;
@@ -828,6 +833,29 @@ int Engine::get_normal_equations(bool user, int n, const int* ents, double* G, d
         Ge[i * K + j] = val;
       }
       ce[i] = i < k ? v[i] : cb;
+    }
+  }
+  return 0;
+}
+
+// CG vectors r, p, q of the side as left by the last solve (K = k+1 per user
+// with the bias entry last, k per item), for tests.
+int Engine::get_cg_vectors(bool user, double* r, double* p, double* q) {
+  MR_HIP(hipSetDevice(device));
+  Side& S = user ? su : si;
+  const int K = user ? k + 1 : k;
+  std::vector<double> v(S.E * ldk), b(user ? S.E : 0);
+  double* outs[3] = {r, p, q};
+  double* vecs[3] = {S.r, S.p, S.q};
+  double* bvs[3] = {S.rb, S.pb, S.qb};
+  for (int t = 0; t < 3; ++t) {
+    if (!outs[t]) continue;
+    MR_HIP(hipMemcpyAsync(v.data(), vecs[t], v.size() * 8, hipMemcpyDeviceToHost, stream));
+    if (user) MR_HIP(hipMemcpyAsync(b.data(), bvs[t], b.size() * 8, hipMemcpyDeviceToHost, stream));
+    MR_HIP(hipStreamSynchronize(stream));
+    for (int64_t e = 0; e < S.E; ++e) {
+      for (int j = 0; j < k; ++j) outs[t][e * K + j] = v[e * ldk + j];
+      if (user) outs[t][e * K + k] = b[e];
     }
   }
   return 0;

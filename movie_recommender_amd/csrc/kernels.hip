@@ -17,15 +17,6 @@
 
 #include "mr_internal.h"
 
-// Tuning switch (build-time; tools/build_variant.sh): row buffers of the
-// Gram main loop (groups in flight + 1).  Measured on MI355X (ML-full shape,
-// k = 64, tools/ab_gram.sh): 4 buffers of G = 2 steps is best.
-#ifndef MR_BF3_ORDER
-#define MR_BF3_ORDER 0   // bf16x3 MFMA order: 0 product-major, 1 block-major
-#endif
-#ifndef MR_GRAM_NBUF
-#define MR_GRAM_NBUF 4
-#endif
 
 namespace mr {
 
@@ -61,63 +52,89 @@ __device__ __forceinline__ double block_sum_f64(double v, double* sh) {
   return t;  // valid on thread 0
 }
 
-constexpr int MV_WAVES = 4;
-constexpr int MV_CST = 68;   // float4 stride of a column-partial row (+16 floats: no bank clash)
+// Cross-lane moves of a double through DPP (two 32-bit halves).  CTRL:
+// quad_perm 0xB1 = lane ^ 1, 0x4E = lane ^ 2 (inside a quad); row_ror 0x124
+// / 0x128 rotate a 16-lane row by 4 / 8.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo);
+}
+// Sum over the 4 lanes of a quad; every lane of the quad gets the same value.
+__device__ __forceinline__ double quad_sum_f64(double v) {
+  v += dpp_f64<0xB1>(v);
+  return v + dpp_f64<0x4E>(v);
+}
+// Sum over the 16 lanes of a row; lanes 0..3 of the row hold the same value,
+// (Q0 + Q3) + (Q2 + Q1) over the row's quad sums Q (other lanes: other orders).
+__device__ __forceinline__ double row_sum_f64(double v) {
+  v = quad_sum_f64(v);
+  v += dpp_f64<0x124>(v);
+  return v + dpp_f64<0x128>(v);
+}
 
-// Per-wave LDS scratch of the tile GEMV (one entity at a time).
+constexpr int MV_WAVES = 4;
+
+// Per-wave LDS scratch of the tile GEMV (one entity at a time).  The CG
+// vectors are fp64 (a fp32 residual / direction breaks CG's recurrences on
+// ill-conditioned blocks: DESIGN.md "Precision"), G is fp32 and every product
+// G_ij v_j is accumulated in fp64.
 template <int NB>
 struct MvScratch {
   static constexpr int NF = NB / 2;
-  float pv[16 * NB];               // the vector, virtual order
-  float redR[NB][64];              // 4-lane row partials
-  float4 redC[NB][MV_CST];         // 16-lane column partials
+  double pv[16 * NB];              // the vector, virtual order
+  double redR[NB][16];             // row sums (quad-reduced in registers)
+  double redC[NB][256];            // 16-lane column partials: [b][16 rr + c]
   float dd[NF > 0 ? 16 * NF : 1];  // side-array diagonals of the folded tiles
 };
 
 // y = G_e v for ONE entity, by one wave, on tri16 tiles already in registers
 // (lane l holds float4 l of every tile: T[l>>2][4(l&3) .. +3]).  Lane l
 // accumulates the row product T v_bj into y_bi and, for bi < bj, the column
-// product T^T v_bi into y_bj; the 4-lane row partials and 16-lane column
-// partials are combined through LDS in a fixed order.  Requires sc.pv (v in
-// virtual order) and sc.dd staged.  Returns y at virtual index lane + 64 h in
-// yo[h] (0 for padding, n >= k) and, user side, the bias row
-// yb = Gs.v + Gn vb (wave-uniform); Gs_e / gn are the entity's row sums and
-// count.  The user-side bias column Gs vb is added to every y.
+// product T^T v_bi into y_bj (fp64); the 4-lane row partials are summed by DPP
+// inside each quad, the 16-lane column partials through LDS, both in a fixed
+// order.  Requires sc.pv (v in virtual order) and sc.dd staged.  Returns y at
+// virtual index lane + 64 h in yo[h] (0 for padding, n >= k) and, user side,
+// the bias row yb = Gs.v + Gn vb (wave-uniform); Gs_e / gn are the entity's row
+// sums and count.  The user-side bias column Gs vb is added to every y.
 template <int NB, bool USER>
 __device__ __forceinline__ void tile_matvec(
-    const float4 (&g)[NB * (NB - 1) / 2 + NB / 2 + (NB & 1)], MvScratch<NB>& sc, float vb,
-    const float* __restrict__ Gs_e, float gn, int k, float (&yo)[(16 * NB + 63) / 64],
-    float& yb) {
+    const float4 (&g)[NB * (NB - 1) / 2 + NB / 2 + (NB & 1)], MvScratch<NB>& sc, double vb,
+    const float* __restrict__ Gs_e, float gn, int k, double (&yo)[(16 * NB + 63) / 64],
+    double& yb) {
   constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2;
   constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
   const int lane = threadIdx.x & 63;
   const int rr = lane >> 2, c4 = (lane & 3) * 4;
-  float accR[NB];
-  float4 accC[NB];
+  double accR[NB];
+  double accC[NB][4];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    accR[b] = 0.f;
-    accC[b] = make_float4(0.f, 0.f, 0.f, 0.f);
+    accR[b] = 0.0;
+#pragma unroll
+    for (int x = 0; x < 4; ++x) accC[b][x] = 0.0;
   }
   // strictly-upper tiles: row product into y_bi, column product into y_bj
   int t = 0;
 #pragma unroll
   for (int bi = 0; bi < NB; ++bi) {
-    const float pi = sc.pv[16 * bi + rr];
+    const double pi = sc.pv[16 * bi + rr];
 #pragma unroll
     for (int bj = bi + 1; bj < NB; ++bj) {
       const float4 gg = g[t];
-      const float4 pj = *reinterpret_cast<const float4*>(&sc.pv[16 * bj + c4]);
-      float s0 = accR[bi];
-      s0 = fmaf(gg.x, pj.x, s0);
-      s0 = fmaf(gg.y, pj.y, s0);
-      s0 = fmaf(gg.z, pj.z, s0);
-      s0 = fmaf(gg.w, pj.w, s0);
+      const double ge[4] = {gg.x, gg.y, gg.z, gg.w};
+      const double2 pa = *reinterpret_cast<const double2*>(&sc.pv[16 * bj + c4]);
+      const double2 pb = *reinterpret_cast<const double2*>(&sc.pv[16 * bj + c4 + 2]);
+      double s0 = accR[bi];
+      s0 = fma(ge[0], pa.x, s0);
+      s0 = fma(ge[1], pa.y, s0);
+      s0 = fma(ge[2], pb.x, s0);
+      s0 = fma(ge[3], pb.y, s0);
       accR[bi] = s0;
-      accC[bj].x = fmaf(gg.x, pi, accC[bj].x);
-      accC[bj].y = fmaf(gg.y, pi, accC[bj].y);
-      accC[bj].z = fmaf(gg.z, pi, accC[bj].z);
-      accC[bj].w = fmaf(gg.w, pi, accC[bj].w);
+#pragma unroll
+      for (int x = 0; x < 4; ++x) accC[bj][x] = fma(ge[x], pi, accC[bj][x]);
       ++t;
     }
   }
@@ -127,77 +144,79 @@ __device__ __forceinline__ void tile_matvec(
   for (int m = 0; m < NF; ++m) {
     const int b0 = 2 * m, b1 = 2 * m + 1;
     const float4 gg = g[NO + m];
-    const float ge[4] = {gg.x, gg.y, gg.z, gg.w};
-    const float4 p0 = *reinterpret_cast<const float4*>(&sc.pv[16 * b0 + c4]);
-    const float4 p1 = *reinterpret_cast<const float4*>(&sc.pv[16 * b1 + c4]);
-    const float p0c[4] = {p0.x, p0.y, p0.z, p0.w};
-    const float p1c[4] = {p1.x, p1.y, p1.z, p1.w};
-    const float pr0 = sc.pv[16 * b0 + rr], pr1 = sc.pv[16 * b1 + rr];
-    float c0[4], c1[4];
+    const double ge[4] = {gg.x, gg.y, gg.z, gg.w};
+    const double pr0 = sc.pv[16 * b0 + rr], pr1 = sc.pv[16 * b1 + rr];
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
       const int c = c4 + x;
-      const float gu = (c >= rr) ? ge[x] : 0.f;
-      const float gc = (c > rr) ? ge[x] : 0.f;
-      const float gl = (c < rr) ? ge[x] : 0.f;
-      accR[b0] = fmaf(gu, p0c[x], accR[b0]);
-      accR[b1] = fmaf(gl, p1c[x], accR[b1]);
-      c0[x] = gc * pr0;
-      c1[x] = gl * pr1;
+      const double gu = (c >= rr) ? ge[x] : 0.0;
+      const double gc = (c > rr) ? ge[x] : 0.0;
+      const double gl = (c < rr) ? ge[x] : 0.0;
+      accR[b0] = fma(gu, sc.pv[16 * b0 + c], accR[b0]);
+      accR[b1] = fma(gl, sc.pv[16 * b1 + c], accR[b1]);
+      accC[b0][x] = fma(gc, pr0, accC[b0][x]);
+      accC[b1][x] = fma(gl, pr1, accC[b1][x]);
     }
-    accC[b0].x += c0[0]; accC[b0].y += c0[1]; accC[b0].z += c0[2]; accC[b0].w += c0[3];
-    accC[b1].x += c1[0]; accC[b1].y += c1[1]; accC[b1].z += c1[2]; accC[b1].w += c1[3];
   }
-  if constexpr ((NB & 1) != 0) {   // last diagonal block stored full: row product
+  if constexpr ((NB & 1) != 0) {
+    // last diagonal block, stored full: only its upper triangle defines G
+    // (the bf16x3 MFMA sum is not bitwise symmetric: B[i][j] and B[j][i] add
+    // the hm / mh products in opposite orders), as in packed_offset
+    const int b0 = NB - 1;
     const float4 gg = g[NO + NF];
-    const float4 pj = *reinterpret_cast<const float4*>(&sc.pv[16 * (NB - 1) + c4]);
-    float s0 = accR[NB - 1];
-    s0 = fmaf(gg.x, pj.x, s0);
-    s0 = fmaf(gg.y, pj.y, s0);
-    s0 = fmaf(gg.z, pj.z, s0);
-    s0 = fmaf(gg.w, pj.w, s0);
-    accR[NB - 1] = s0;
+    const double ge[4] = {gg.x, gg.y, gg.z, gg.w};
+    const double pr0 = sc.pv[16 * b0 + rr];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const int c = c4 + x;
+      const double gu = (c >= rr) ? ge[x] : 0.0;
+      const double gc = (c > rr) ? ge[x] : 0.0;
+      accR[b0] = fma(gu, sc.pv[16 * b0 + c], accR[b0]);
+      accC[b0][x] = fma(gc, pr0, accC[b0][x]);
+    }
   }
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    sc.redR[b][lane] = accR[b];
-    sc.redC[b][lane] = accC[b];
+    const double rs = quad_sum_f64(accR[b]);
+    if ((lane & 3) == 0) sc.redR[b][rr] = rs;
+    double2* dst = reinterpret_cast<double2*>(&sc.redC[b][4 * lane]);
+    dst[0] = make_double2(accC[b][0], accC[b][1]);
+    dst[1] = make_double2(accC[b][2], accC[b][3]);
   }
   __builtin_amdgcn_wave_barrier();
-  float ybp = 0.f;
+  double ybp = 0.0;
 #pragma unroll
   for (int h = 0; h < NV; ++h) {
     const int o = lane + 64 * h;   // virtual index
-    yo[h] = 0.f;
+    yo[h] = 0.0;
     if (o >= NP) continue;
     const int n = nat_of(o, NB);
     if (n >= k) continue;
     const int b = o >> 4, ii = o & 15;
-    const float* R = &sc.redR[b][4 * ii];
-    float y = (R[0] + R[1]) + (R[2] + R[3]);
-    const float* C = reinterpret_cast<const float*>(&sc.redC[b][0]) + ii;
-    float s = 0.f;
+    const double* C = &sc.redC[b][ii];
+    double s[4];
 #pragma unroll
-    for (int qq = 0; qq < 16; ++qq) s += C[16 * qq];
-    y += s;
-    if (NF > 0 && (b & 1) && b < 2 * NF) y = fmaf(sc.dd[(b >> 1) * 16 + ii], sc.pv[o], y);
+    for (int j = 0; j < 4; ++j)
+      s[j] = (C[16 * (4 * j)] + C[16 * (4 * j + 1)]) + (C[16 * (4 * j + 2)] + C[16 * (4 * j + 3)]);
+    double y = sc.redR[b][ii] + ((s[0] + s[1]) + (s[2] + s[3]));
+    if (NF > 0 && (b & 1) && b < 2 * NF) y = fma((double)sc.dd[(b >> 1) * 16 + ii], sc.pv[o], y);
     if (USER) {
-      const float gs = Gs_e[n];
-      y = fmaf(gs, vb, y);
-      ybp = fmaf(gs, sc.pv[o], ybp);
+      const double gs = Gs_e[n];
+      y = fma(gs, vb, y);
+      ybp = fma(gs, sc.pv[o], ybp);
     }
     yo[h] = y;
   }
-  if (USER) yb = fmaf(gn, vb, wave_sum_f32(ybp));
+  if (USER) yb = fma((double)gn, vb, wave_sum_f64(ybp));
 }
 
 // CG start for ONE entity, by one wave, in block form (cg_least_squares,
 // matrix.cpp:464-476 and the first matvec / dot of its loop, :493-497):
 //   r0 = G x - c,  p0 = -r0,  q0 = G p0
-// written to the CG vectors; this wave's lanes add r0.r0 to drr and p0.q0 to
-// dpq (fp64; callers reduce in a fixed order).  G / Gs / Gn / C / Cb hold the
-// entity's finished normal equations (read back through L2 right after the
-// Gram wave stored them, or after slab_reduce for split entities).
+// written to the (fp64) CG vectors; this wave's lanes add r0.r0 to drr and
+// p0.q0 to dpq (callers reduce in a fixed order).  G / Gs / Gn / C / Cb hold
+// the entity's finished normal equations (after slab_reduce for split
+// entities).
 template <int NB, bool USER>
 __device__ __forceinline__ void cg_start_entity(int64_t e, int k, int ldk,
                                                 const GramDst& D, const CgStart& cs,
@@ -214,8 +233,8 @@ __device__ __forceinline__ void cg_start_entity(int64_t e, int k, int ldk,
     xv[h] = (i < NP) ? cs.x[e * ldk + i] : 0.f;
     cn[h] = (i < NP) ? D.C[e * D.sV + nat_of(i, NB)] : 0.f;
   }
-  const float xb = USER ? cs.xb[e] : 0.f;
-  const float cb = USER ? D.Cb[e * D.sS] : 0.f;
+  const double xb = USER ? (double)cs.xb[e] : 0.0;
+  const double cb = USER ? (double)D.Cb[e * D.sS] : 0.0;
   const float gn = USER ? D.Gn[e * D.sS] : 0.f;
   const float* Gs_e = USER ? D.Gs + e * D.sV : nullptr;
   const float4* __restrict__ Ge = reinterpret_cast<const float4*>(D.G + e * D.sG);
@@ -229,7 +248,7 @@ __device__ __forceinline__ void cg_start_entity(int64_t e, int k, int ldk,
     if (i < NP) sc.pv[virt_of(i, NB)] = xv[h];
   }
   __builtin_amdgcn_wave_barrier();
-  float yo[NV], yb = 0.f;
+  double yo[NV], yb = 0.0;
   tile_matvec<NB, USER>(g, sc, xb, Gs_e, gn, k, yo, yb);
   __builtin_amdgcn_wave_barrier();
   // r0 = G x - c, p0 = -r0 (:468-476); p0 replaces x in LDS
@@ -239,25 +258,25 @@ __device__ __forceinline__ void cg_start_entity(int64_t e, int k, int ldk,
     const int o = lane + 64 * h;
     if (o < NP) {
       const int n = nat_of(o, NB);
-      float pn = 0.f;
+      double pn = 0.0;
       if (n < k) {
-        const float rv = yo[h] - cn[h];
+        const double rv = yo[h] - (double)cn[h];
         cs.r[e * ldk + n] = rv;
         cs.p[e * ldk + n] = -rv;
-        d += (double)rv * rv;
+        d = fma(rv, rv, d);
         pn = -rv;
       }
       sc.pv[o] = pn;
     }
   }
-  float pb = 0.f;
+  double pb = 0.0;
   if (USER) {
-    const float rbv = yb - cb;
+    const double rbv = yb - cb;
     pb = -rbv;
     if (lane == 0) {
       cs.rb[e] = rbv;
       cs.pb[e] = pb;
-      d += (double)rbv * rbv;
+      d = fma(rbv, rbv, d);
     }
   }
   drr += wave_sum_f64(d);
@@ -272,13 +291,13 @@ __device__ __forceinline__ void cg_start_entity(int64_t e, int k, int ldk,
       const int n = nat_of(o, NB);
       if (n < k) {
         cs.q[e * ldk + n] = yo[h];
-        d += (double)yo[h] * sc.pv[o];
+        d = fma(yo[h], sc.pv[o], d);
       }
     }
   }
   if (USER && lane == 0) {
     cs.qb[e] = yb;
-    d += (double)yb * pb;
+    d = fma(yb, pb, d);
   }
   dpq += wave_sum_f64(d);
   __builtin_amdgcn_wave_barrier();
@@ -326,76 +345,92 @@ __device__ __forceinline__ void load_row_seg(float (&v)[NB], const float* __rest
 }
 
 // Per-wave LDS of the accumulator-based CG start (start_from_acc).
-constexpr int SR_STRIDE = 68;   // row-partial stride (floats): 4 r-rows hit distinct banks
 template <int NB>
 struct StartScratch {
-  float pv[16 * NB];                 // the vector, virtual order
+  double pv[16 * NB];                // the vector, virtual order
+  double yR[16 * NB];                // row-product sums
+  double yC[16 * NB];                // column-product sums
   float sC[16 * NB];                 // rhs c, virtual order
   float sGs[16 * NB];                // user side: row sums, virtual order
-  float partR[NB * 4][SR_STRIDE];    // [4 bi + r][lane]: row-product partials
-  float partC[NB][64];               // [bj][lane]: column-product partials
 };
 
 // y = G v straight from the MFMA accumulators of the Gram wave (no memory
-// round trip).  acc[t(bi,bj)] (bi <= bj, diagonal blocks FULL) holds
-// B[4q + r][col] in lane (q, col).  Row products B v_bj go to y_bi (summed
-// over the 16 lanes of a q-group), column products B^T v_bi of the
-// off-diagonal blocks to y_bj (summed over the 4 q-groups), both through LDS
-// in a fixed order.  v in sc.pv (virtual order).  Returns y at virtual
-// o = lane + 64 h in yo[h] (without the bias column) -- 0 for padding.
+// round trip), products accumulated in fp64.  acc[t(bi,bj)] (bi <= bj,
+// diagonal blocks FULL) holds B[4q + r][col] in lane (q, col).  Row products
+// B v_bj go to y_bi (summed over the 16 lanes of row q by DPP), column
+// products B^T v_bi to y_bj (summed over the 4 rows by lane shuffles), both
+// in a fixed order; a diagonal block contributes its stored triangle only.  v in sc.pv (virtual order).
+// Returns y at virtual o = lane + 64 h in yo[h] (without the bias column) --
+// 0 for padding.
 template <int NB>
 __device__ __forceinline__ void acc_matvec(const floatx4 (&acc)[NB * (NB + 1) / 2],
                                            StartScratch<NB>& sc, int k,
-                                           float (&yo)[(16 * NB + 63) / 64]) {
+                                           double (&yo)[(16 * NB + 63) / 64]) {
   constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
   const int lane = threadIdx.x & 63, q = lane >> 4, col = lane & 15;
-  float R[NB][4], Cp[NB];
+  double R[NB][4], Cp[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    Cp[b] = 0.f;
+    Cp[b] = 0.0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) R[b][r] = 0.f;
+    for (int r = 0; r < 4; ++r) R[b][r] = 0.0;
   }
   int t = 0;
 #pragma unroll
   for (int bi = 0; bi < NB; ++bi) {
-    const float4 vq = *reinterpret_cast<const float4*>(&sc.pv[16 * bi + 4 * q]);
+    const double2 va = *reinterpret_cast<const double2*>(&sc.pv[16 * bi + 4 * q]);
+    const double2 vb = *reinterpret_cast<const double2*>(&sc.pv[16 * bi + 4 * q + 2]);
 #pragma unroll
     for (int bj = bi; bj < NB; ++bj) {
-      const float vj = sc.pv[16 * bj + col];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) R[bi][r] = fmaf(acc[t][r], vj, R[bi][r]);
+      const double vj = sc.pv[16 * bj + col];
+      const double a[4] = {acc[t][0], acc[t][1], acc[t][2], acc[t][3]};
+      const double vr[4] = {va.x, va.y, vb.x, vb.y};   // v_bi at rows 4q + r
       if (bi != bj) {
-        float c = Cp[bj];
-        c = fmaf(acc[t][0], vq.x, c);
-        c = fmaf(acc[t][1], vq.y, c);
-        c = fmaf(acc[t][2], vq.z, c);
-        c = fmaf(acc[t][3], vq.w, c);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) R[bi][r] = fma(a[r], vj, R[bi][r]);
+        double c = Cp[bj];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) c = fma(a[r], vr[r], c);
         Cp[bj] = c;
+      } else {
+        // diagonal block: the bf16x3 sum is not bitwise symmetric, so use
+        // exactly the triangle tri16 stores (upper for even blocks and the
+        // odd last block, lower + side diagonal for odd folded blocks) for
+        // both the row and the transposed product, as the GEMV does
+        const bool lower = (bi & 1) && !((NB & 1) && bi == NB - 1);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 4 * q + r;
+          const bool rowuse = lower ? (col <= row) : (col >= row);
+          const bool coluse = lower ? (col < row) : (col > row);
+          R[bi][r] = fma(rowuse ? a[r] : 0.0, vj, R[bi][r]);
+          Cp[bi] = fma(coluse ? a[r] : 0.0, vr[r], Cp[bi]);
+        }
       }
       ++t;
     }
   }
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
+    double rs[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) sc.partR[4 * b + r][lane] = R[b][r];
-    sc.partC[b][lane] = Cp[b];
+    for (int r = 0; r < 4; ++r) rs[r] = row_sum_f64(R[b][r]);
+    // lanes 0..3 of row q hold identical row sums: lane (q, r) stores row 4q + r
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (col == r) sc.yR[16 * b + 4 * q + r] = rs[r];
+    double c = Cp[b];
+    c += __shfl_xor(c, 16, 64);
+    c += __shfl_xor(c, 32, 64);   // identical in all 4 rows
+    if (q == 0) sc.yC[16 * b + col] = c;
   }
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int h = 0; h < NV; ++h) {
     const int o = lane + 64 * h;
-    yo[h] = 0.f;
+    yo[h] = 0.0;
     if (o >= NP || nat_of(o, NB) >= k) continue;
-    const int b = o >> 4, i = o & 15, qq = i >> 2, rr = i & 3;
-    const float4* pr = reinterpret_cast<const float4*>(&sc.partR[4 * b + rr][16 * qq]);
-    const float4 a0 = pr[0], a1 = pr[1], a2 = pr[2], a3 = pr[3];
-    const float s0 = ((a0.x + a0.y) + (a0.z + a0.w)) + ((a1.x + a1.y) + (a1.z + a1.w));
-    const float s1 = ((a2.x + a2.y) + (a2.z + a2.w)) + ((a3.x + a3.y) + (a3.z + a3.w));
-    const float c = (sc.partC[b][i] + sc.partC[b][16 + i]) +
-                    (sc.partC[b][32 + i] + sc.partC[b][48 + i]);
-    yo[h] = (s0 + s1) + c;
+    yo[h] = sc.yR[o] + sc.yC[o];
   }
   __builtin_amdgcn_wave_barrier();
 }
@@ -403,7 +438,7 @@ __device__ __forceinline__ void acc_matvec(const floatx4 (&acc)[NB * (NB + 1) / 
 // Fused CG start of one unsplit entity from the Gram wave's registers
 // (cg_least_squares, matrix.cpp:464-476 and iteration 0's matvec / dot,
 // :493-497, in block form): r0 = G x - c, p0 = -r0, q0 = G p0, written to
-// the CG vectors; adds r0.r0 to drr and p0.q0 to dpq (fp64, lane partials
+// the fp64 CG vectors; adds r0.r0 to drr and p0.q0 to dpq (lane partials
 // summed across the wave).  cacc / sacc: c and the row sums at virtual
 // (b, col) in every lane (already reduced over q); wt / gn: user-side
 // sum of ratings and count; xv / xb: x at virtual (b, col) and its bias.
@@ -426,40 +461,40 @@ __device__ __forceinline__ void start_from_acc(const floatx4 (&acc)[NB * (NB + 1
     }
   }
   __builtin_amdgcn_wave_barrier();
-  float yo[NV];
+  double yo[NV];
   acc_matvec<NB>(acc, sc, k, yo);
   // r0 = G x - c (+ bias column), p0 = -r0; user bias row: Gs.x + Gn xb - Cb
-  double d = 0.0;
-  float ybp = 0.f, pn[NV];
+  const double xbd = xb;
+  double d = 0.0, ybp = 0.0, pn[NV];
 #pragma unroll
   for (int h = 0; h < NV; ++h) {
     const int o = lane + 64 * h;
-    pn[h] = 0.f;
+    pn[h] = 0.0;
     if (o < NP) {
       const int n = nat_of(o, NB);
       if (n < k) {
-        float y = yo[h];
+        double y = yo[h];
         if (USER) {
-          const float gs = sc.sGs[o];
-          y = fmaf(gs, xb, y);
-          ybp = fmaf(gs, sc.pv[o], ybp);
+          const double gs = sc.sGs[o];
+          y = fma(gs, xbd, y);
+          ybp = fma(gs, sc.pv[o], ybp);
         }
-        const float rv = y - sc.sC[o];
+        const double rv = y - (double)sc.sC[o];
         cs.r[e * ldk + n] = rv;
         cs.p[e * ldk + n] = -rv;
-        d += (double)rv * rv;
+        d = fma(rv, rv, d);
         pn[h] = -rv;
       }
     }
   }
-  float pb = 0.f;
+  double pb = 0.0;
   if (USER) {
-    const float rbv = fmaf(gn, xb, wave_sum_f32(ybp)) - wt;
+    const double rbv = fma((double)gn, xbd, wave_sum_f64(ybp)) - (double)wt;
     pb = -rbv;
     if (lane == 0) {
       cs.rb[e] = rbv;
       cs.pb[e] = pb;
-      d += (double)rbv * rbv;
+      d = fma(rbv, rbv, d);
     }
   }
   drr += wave_sum_f64(d);
@@ -473,29 +508,29 @@ __device__ __forceinline__ void start_from_acc(const floatx4 (&acc)[NB * (NB + 1
   // q0 = G p0 (+ bias column), p0.q0
   acc_matvec<NB>(acc, sc, k, yo);
   d = 0.0;
-  ybp = 0.f;
+  ybp = 0.0;
 #pragma unroll
   for (int h = 0; h < NV; ++h) {
     const int o = lane + 64 * h;
     if (o < NP) {
       const int n = nat_of(o, NB);
       if (n < k) {
-        float y = yo[h];
+        double y = yo[h];
         if (USER) {
-          const float gs = sc.sGs[o];
-          y = fmaf(gs, pb, y);
-          ybp = fmaf(gs, pn[h], ybp);
+          const double gs = sc.sGs[o];
+          y = fma(gs, pb, y);
+          ybp = fma(gs, pn[h], ybp);
         }
         cs.q[e * ldk + n] = y;
-        d += (double)y * pn[h];
+        d = fma(y, pn[h], d);
       }
     }
   }
   if (USER) {
-    const float qb = fmaf(gn, pb, wave_sum_f32(ybp));
+    const double qb = fma((double)gn, pb, wave_sum_f64(ybp));
     if (lane == 0) {
       cs.qb[e] = qb;
-      d += (double)qb * pb;
+      d = fma(qb, pb, d);
     }
   }
   dpq += wave_sum_f64(d);
@@ -504,26 +539,33 @@ __device__ __forceinline__ void start_from_acc(const floatx4 (&acc)[NB * (NB + 1
 // ---------------------------------------------------------------------------
 // K1: gather-Gram.  One wave per WorkItem (an entity, or a chunk of a heavy
 // entity).  Rows a_r are gathered from the opposite factor table (row stride
-// ldk floats) and accumulated with v_mfma_f32_16x16x4_f32: lane l supplies
-// a_{r0+(l>>4)}[16b + (l&15)], which is both the A operand (A[i][kk],
-// i = l&15, kk = l>>4) and the B operand (B[kk][j], j = l&15) of block
-// (bi, bj): D += A_bi^T A_bj over 4 ratings per MFMA.  Only the NB(NB+1)/2
-// upper blocks are computed (k = 64: 10 of 16), and the accumulators are
-// stored as they stand: D[row = 4(l>>4) + reg][col = l&15] is exactly the
-// row-major tile layout of tri16 storage, so the epilogue needs no transpose
-// (diagonal blocks are masked into their folded tile / side array).  The rhs and
-// (user side) row sums / counts ride along on VALU.  Item side:
-// w = r - U[u][k] (fill_ratings_minus_bias, :1021-1030).
-// Rows of UNR steps are gathered before their MFMAs (UNR*NB loads in flight
-// per wave).
+// ldk floats) and accumulated on the matrix cores with
+// v_mfma_f32_16x16x32_bf16 in an exact bf16x3 split (below).  Only the
+// NB(NB+1)/2 upper 16 x 16 blocks are computed (k = 64: 10 of 16), and the
+// accumulators are stored as they stand: D[row = 4(l>>4) + reg][col = l&15]
+// is exactly the row-major tile layout of tri16 storage, so the epilogue needs
+// no transpose (diagonal blocks are masked into their folded tile / side
+// array).  The rhs and (user side) row sums / counts ride along on VALU.
+// Item side: w = r - U[u][k] (fill_ratings_minus_bias, :1021-1030).
+//
+// bf16x3: v_mfma_f32_16x16x32_bf16 takes, in lane (q, col), 8 consecutive K
+// values of row / column col.  With K = ratings that is "ratings 8q .. 8q+7
+// of virtual column 16b + col", which is what lane (q, col) holds after
+// gathering rows 8q + t (t < 8) of a 32-rating half with its NB-float
+// segment per row: the operands need no transpose.  Each float is split
+// EXACTLY into three bf16 by truncation (h = top 16 bits, m = top 16 bits of
+// a - h, l = a - h - m, which has <= 8 significant bits), and each block
+// accumulates the six products of weight >= 2^-16 of h h^T: hh + hm + mh +
+// hl + lh + mm (the dropped ml, lm, ll are <= 2^-24 relative, below the fp32
+// rounding of the sum).
 // ---------------------------------------------------------------------------
 constexpr int GRAM_WAVES = 4;
 
-// Per-lane raw loads of one 64-rating chunk: opposite id, rating and (item
+// Per-lane raw loads of one 32-rating half: opposite id, rating and (item
 // side) the opposite bias.  Lanes past the end of the work item load from a
-// safe in-range address; finish_raw masks them (id -> the all-zero row
-// `zrow`, weight 0) only when the chunk becomes current, so no select waits
-// on a load that was just issued.
+// safe in-range address and are masked (id -> the all-zero row `zrow`,
+// weight 0) only when the half becomes current, so no select waits on a load
+// that was just issued.
 struct ChunkRaw {
   int idx;
   float r;
@@ -534,138 +576,14 @@ struct ChunkRegs {
   float w;
 };
 
-__device__ __forceinline__ ChunkRaw load_chunk_raw(const int32_t* __restrict__ idx,
-                                                   const float* __restrict__ val,
-                                                   int64_t begin, int64_t end, int64_t safe,
-                                                   int c, int lane) {
-  const int64_t jj = begin + 64 * (int64_t)c + lane;
-  const int64_t js = jj < end ? jj : safe;
-  ChunkRaw r;
-  r.idx = idx[js];
-  r.r = val[js];
-  r.b = 0.f;
-  return r;
-}
-
-// Item side: the opposite bias, gathered through ids loaded one chunk earlier
-// (masked lanes read bias[zrow] == 0).
-template <bool USER>
-__device__ __forceinline__ void load_bias_raw(ChunkRaw& c, const float* __restrict__ bias,
-                                              int64_t begin, int64_t end, int ci, int lane,
-                                              int zrow) {
-  if (!USER) {
-    const bool ok = begin + 64 * (int64_t)ci + lane < end;
-    c.b = bias[ok ? c.idx : zrow];
-  }
-}
-
-__device__ __forceinline__ ChunkRegs finish_raw(const ChunkRaw& c, int64_t begin, int64_t end,
-                                                int ci, int lane, int zrow) {
-  const bool ok = begin + 64 * (int64_t)ci + lane < end;
-  ChunkRegs r;
-  r.idx = ok ? c.idx : zrow;
-  r.w = ok ? c.r - c.b : 0.f;
-  return r;
-}
-
-// Gather the rows of G steps (4 ratings each) into registers.  Lane l takes
-// row (l>>4) of each step and its NB contiguous floats starting at natural
-// column NB*(l&15): a[u][b] = F[row][NB*(l&15) + b] is the operand of virtual
-// block b (k = 64: one dwordx4 per lane, a 1-KiB wave-instruction = 4 whole
-// rows).  Fc is the lane's column base, one v_mad_u64_u32 per row address.
-template <int NB, int G>
-__device__ __forceinline__ void gather_group(float (&a)[G][NB], float (&ww)[G], ChunkRegs cr,
-                                             int step0_in_chunk, const char* __restrict__ Fc,
-                                             uint32_t row_bytes, int q) {
-#pragma unroll
-  for (int u = 0; u < G; ++u) {
-    const int src = 4 * (step0_in_chunk + u) + q;
-#if defined(MR_GRAM_PROBE) && MR_GRAM_PROBE == 1
-    const int ri = __shfl(cr.idx, src, 64) & 1023;   // probe: cache-resident rows
-#else
-    const int ri = __shfl(cr.idx, src, 64);
-#endif
-    ww[u] = __shfl(cr.w, src, 64);
-    const char* p = Fc + (uint64_t)(uint32_t)ri * row_bytes;
-#if defined(MR_GRAM_PROBE) && MR_GRAM_PROBE == 3
-    // probe: no gathers (operands derived from the chunk registers)
-#pragma unroll
-    for (int b = 0; b < NB; ++b) a[u][b] = __int_as_float(ri) * (float)(b + 1);
-    continue;
-#endif
-    if constexpr (NB % 4 == 0) {
-#pragma unroll
-      for (int h = 0; h < NB / 4; ++h) {
-        const float4 v = *reinterpret_cast<const float4*>(p + 16 * h);
-        a[u][4 * h + 0] = v.x;
-        a[u][4 * h + 1] = v.y;
-        a[u][4 * h + 2] = v.z;
-        a[u][4 * h + 3] = v.w;
-      }
-    } else if constexpr (NB % 2 == 0) {
-#pragma unroll
-      for (int h = 0; h < NB / 2; ++h) {
-        const float2 v = *reinterpret_cast<const float2*>(p + 8 * h);
-        a[u][2 * h + 0] = v.x;
-        a[u][2 * h + 1] = v.y;
-      }
-    } else {
-#pragma unroll
-      for (int b = 0; b < NB; ++b) a[u][b] = *reinterpret_cast<const float*>(p + 4 * b);
-    }
-  }
-}
-
-template <int NB, int G, bool USER>
-__device__ __forceinline__ void mfma_group(floatx4 (&acc)[NB * (NB + 1) / 2],
-                                           float (&cacc)[NB], float (&sacc)[NB], float& wsum,
-                                           const float (&a)[G][NB], const float (&ww)[G],
-                                           int steps_left) {
-  // one scalar test per group: a partial group's missing steps gathered the
-  // all-zero row with weight 0, so their MFMAs add exact zeros (per-step
-  // tests split the group into blocks that defeat register reuse)
-  if (steps_left <= 0) return;
-#pragma unroll
-  for (int u = 0; u < G; ++u) {
-    {
-      int t = 0;
-#pragma unroll
-      for (int bi = 0; bi < NB; ++bi)
-#pragma unroll
-        for (int bj = bi; bj < NB; ++bj) {
-#if defined(MR_GRAM_PROBE) && MR_GRAM_PROBE == 2
-          acc[t][0] += a[u][bi] * a[u][bj];   // probe: no MFMA
-#else
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][bi], a[u][bj], acc[t], 0, 0, 0);
-#endif
-          ++t;
-        }
-    }
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      cacc[b] = fmaf(a[u][b], ww[u], cacc[b]);
-      if (USER) sacc[b] += a[u][b];
-    }
-    if (USER) wsum += ww[u];
-  }
-}
-
-// ---- bf16x3 main loop pieces --------------------------------------------
-// v_mfma_f32_16x16x32_bf16 takes, in lane (q, col), 8 consecutive K values of
-// row / column col.  With K = ratings that is "ratings 8q .. 8q+7 of virtual
-// column 16b + col", which is what lane (q, col) holds after gathering rows
-// 8q + t (t < 8) of a 32-rating half with its NB-float segment per row (the
-// f32 kernel's gather, 8 rows per lane instead of 1 per step): the operands
-// need no transpose.  Each float is split EXACTLY into three bf16 by
-// truncation (h = top 16 bits, m = top 16 bits of a - h, l = a - h - m, which
-// has <= 8 significant bits), and each block accumulates the six products of
-// weight >= 2^-16 of h h^T: hh + hm + mh + hl + lh + mm (dropped ml, lm, ll
-// are <= 2^-24 relative, below fp32 rounding of the sum).
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
+// Lane (q, col) gathers rows 8q .. 8q+7 of half `half` (ids / weights
+// broadcast from lanes 32 half + 8q + t), NB contiguous floats each from its
+// column base Fc (natural columns NB col .. NB col + NB-1 = virtual (b, col)).
 template <int NB>
 __device__ __forceinline__ void gather_half(float (&f)[8][NB], float (&w)[8], ChunkRegs cr,
                                             int half, const char* __restrict__ Fc,
@@ -675,11 +593,6 @@ __device__ __forceinline__ void gather_half(float (&f)[8][NB], float (&w)[8], Ch
     const int src = 32 * half + 8 * q + t;
     const int ri = __shfl(cr.idx, src, 64);
     w[t] = __shfl(cr.w, src, 64);
-#if defined(MR_GRAM_PROBE) && MR_GRAM_PROBE == 3
-#pragma unroll
-    for (int b = 0; b < NB; ++b) f[t][b] = __int_as_float(ri) * (float)(b + 1);
-    continue;
-#endif
     load_row_seg<NB>(f[t], reinterpret_cast<const float*>(Fc + (uint64_t)(uint32_t)ri * row_bytes));
   }
 }
@@ -717,11 +630,11 @@ __device__ __forceinline__ void bf3_split(u32x4_t (&P)[3][NB], float (&cacc)[NB]
   }
 }
 
-// hh, hm, mh, hl, lh, mm over the NB(NB+1)/2 upper blocks
+// hh, hm, mh, hl, lh, mm over the NB(NB+1)/2 upper blocks, product-major
+// (consecutive MFMAs write different accumulators: no dependency stalls).
 template <int NB>
 __device__ __forceinline__ void bf3_mfma(floatx4 (&acc)[NB * (NB + 1) / 2],
                                          const u32x4_t (&P)[3][NB]) {
-#if MR_BF3_ORDER == 0
 #pragma unroll
   for (int sidx = 0; sidx < 6; ++sidx) {
     const int pa = (sidx == 2) ? 1 : (sidx == 4) ? 2 : (sidx == 5) ? 1 : 0;
@@ -737,28 +650,9 @@ __device__ __forceinline__ void bf3_mfma(floatx4 (&acc)[NB * (NB + 1) / 2],
         ++t;
       }
   }
-#else
-  int t = 0;
-#pragma unroll
-  for (int bi = 0; bi < NB; ++bi)
-#pragma unroll
-    for (int bj = bi; bj < NB; ++bj) {
-      floatx4 a = acc[t];
-#pragma unroll
-      for (int sidx = 0; sidx < 6; ++sidx) {
-        const int pa = (sidx == 2) ? 1 : (sidx == 4) ? 2 : (sidx == 5) ? 1 : 0;
-        const int pb = (sidx == 1) ? 1 : (sidx == 3) ? 2 : (sidx == 5) ? 1 : 0;
-        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, P[pa][bi]),
-                                                    __builtin_bit_cast(bf16x8_t, P[pb][bj]), a,
-                                                    0, 0, 0);
-      }
-      acc[t] = a;
-      ++t;
-    }
-#endif
 }
 
-template <int NB, int G, bool USER, bool NTS, bool FUSE>
+template <int NB, bool USER, bool FUSE>
 __device__ __forceinline__ void gram_wave(
     int64_t wi, const WorkItem* __restrict__ work,
     const int32_t* __restrict__ idx, const float* __restrict__ val,
@@ -766,8 +660,6 @@ __device__ __forceinline__ void gram_wave(
     const GramDst& direct, const GramDst& slab, const CgStart& cs, StartScratch<NB>* ssc,
     double& drr, double& dpq) {
   constexpr int T = NB * (NB + 1) / 2;
-  constexpr bool BF3 = (G == 0);           // bf16x3 matrix-core path
-  constexpr int GPC = BF3 ? 2 : 16 / G;    // groups per 64-rating chunk
   const int lane = threadIdx.x & 63;
   // work-item fields in SGPRs: all control flow below is scalar
   const int64_t wbeg = work[wi].begin;
@@ -776,7 +668,6 @@ __device__ __forceinline__ void gram_wave(
   const int wslab = work[wi].slab;
   const int q = lane >> 4, col = lane & 15;
   const int64_t end = wbeg + wlen;
-  const int nst = (wlen + 3) >> 2;              // steps of 4 ratings
   const uint32_t row_bytes = (uint32_t)ldk * 4u;
   const char* Fc = reinterpret_cast<const char*>(F) + 4 * NB * col;
 
@@ -798,110 +689,56 @@ __device__ __forceinline__ void gram_wave(
   for (int b = 0; b < NB; ++b) { cacc[b] = 0.f; sacc[b] = 0.f; }
   float wsum = 0.f;
 
-  // Chunk pipeline (64 ratings per chunk): cur (in use), nxt (ids, ratings
-  // and bias loaded), nx2 (ids and ratings loaded; its bias gather is issued
-  // when it becomes nxt).  Raw loads are masked only when their chunk
-  // becomes current, so no select waits on a load that was just issued.
-  // Every row gather is unconditional (slots past the end read the zero
-  // row), so loads land directly in the buffer registers without merges.
+  // Main loop: one iteration = one 32-rating half with its own id / weight
+  // registers (lanes 0..31; lanes 32..63 mirror them), so the loop body is
+  // uniform: ONE split site and ONE MFMA site (two call sites per iteration
+  // made the compiler rotate the accumulators through extra AGPRs every
+  // iteration).  The half's rows land in F; once split into P (and the rhs
+  // taken), F is refilled with the next half while P's MFMAs run.  Rows past
+  // the end are the zero row with weight 0.  F is loaded and consumed inside
+  // one iteration and only VALU results (P) cross the back-edge, so no
+  // register copy there ever waits on a load in flight.
   const int64_t safe = wlen > 0 ? wbeg : 0;    // an address every wave may read
-  ChunkRaw c0 = load_chunk_raw(idx, val, wbeg, end, safe, 0, lane);
-  ChunkRaw nxt = load_chunk_raw(idx, val, wbeg, end, safe, 1, lane);
-  ChunkRaw nx2 = load_chunk_raw(idx, val, wbeg, end, safe, 2, lane);
-  load_bias_raw<USER>(c0, bias, wbeg, end, 0, lane, zrow);
-  load_bias_raw<USER>(nxt, bias, wbeg, end, 1, lane, zrow);
-  ChunkRegs cur = finish_raw(c0, wbeg, end, 0, lane, zrow);
-  if constexpr (!BF3) {
-  // One loop iteration = one chunk (GPC groups).  NBUF row buffers, group j
-  // of a chunk in buffer j % NBUF (NBUF divides GPC, so the mapping is the
-  // same every chunk and nothing is copied at the back-edge); the rows of
-  // group j + NBUF - 1 are gathered while group j's MFMAs run, so NBUF - 1
-  // groups are in flight.
-  constexpr int NBUF = (MR_GRAM_NBUF < GPC) ? MR_GRAM_NBUF : GPC;
-  constexpr int DIST = NBUF - 1;
-  static_assert(GPC % NBUF == 0, "buffers must tile a chunk");
-  constexpr int GG = BF3 ? 1 : G;
-  float ab[NBUF][GG][NB], wb[NBUF][GG];
-#pragma unroll
-  for (int j = 0; j < DIST; ++j) gather_group<NB, GG>(ab[j], wb[j], cur, j * GG, Fc, row_bytes, q);
-  const int nchunks = (wlen + 63) >> 6;
-  for (int c = 0; c < nchunks; ++c) {
-    ChunkRegs nxtr = cur;
-#pragma unroll
-    for (int j = 0; j < GPC; ++j) {
-      const int jn = j + DIST;   // group gathered now (>= GPC: next chunk)
-      if (jn < GPC) {
-        gather_group<NB, GG>(ab[jn % NBUF], wb[jn % NBUF], cur, jn * GG, Fc, row_bytes, q);
-      } else {
-        if (jn == GPC) nxtr = finish_raw(nxt, wbeg, end, c + 1, lane, zrow);
-        gather_group<NB, GG>(ab[jn % NBUF], wb[jn % NBUF], nxtr, (jn - GPC) * GG, Fc,
-                             row_bytes, q);
-      }
-      mfma_group<NB, GG, USER>(acc, cacc, sacc, wsum, ab[j % NBUF], wb[j % NBUF],
-                               nst - (c * GPC + j) * GG);
-      // this buffer is dead from here: keep its last readers (the rhs FMAs)
-      // above its refill, so the refill reuses its registers
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    cur = nxtr;
-    nxt = nx2;
-    load_bias_raw<USER>(nxt, bias, wbeg, end, c + 2, lane, zrow);
-    nx2 = load_chunk_raw(idx, val, wbeg, end, safe, c + 3, lane);
-  }
-
-  } else {
-    // bf16x3 main loop: one iteration = one 32-rating half with its own
-    // id / weight registers (lanes 0..31; lanes 32..63 mirror them), so the
-    // loop body is uniform: ONE split site and ONE MFMA site (two call sites
-    // per iteration made the compiler rotate the accumulators through extra
-    // AGPRs every iteration).  The half's rows land in F; once split into P
-    // (and the rhs taken), F is refilled with the next half while P's 60
-    // MFMAs run.  Rows past the end are the zero row with weight 0.
-    auto ld32 = [&](int c) {
-      const int64_t jj = wbeg + 32 * (int64_t)c + (lane & 31);
-      ChunkRaw r;
-      const int64_t js = jj < end ? jj : safe;
-      r.idx = idx[js];
-      r.r = val[js];
-      r.b = 0.f;
-      return r;
-    };
-    auto bias32 = [&](ChunkRaw& cr, int c) {
-      if (!USER) {
-        const bool ok = wbeg + 32 * (int64_t)c + (lane & 31) < end;
-        cr.b = bias[ok ? cr.idx : zrow];
-      }
-    };
-    auto fin32 = [&](const ChunkRaw& cr, int c) {
+  auto ld32 = [&](int c) {
+    const int64_t jj = wbeg + 32 * (int64_t)c + (lane & 31);
+    ChunkRaw r;
+    const int64_t js = jj < end ? jj : safe;
+    r.idx = idx[js];
+    r.r = val[js];
+    r.b = 0.f;
+    return r;
+  };
+  auto bias32 = [&](ChunkRaw& cr, int c) {
+    if (!USER) {
       const bool ok = wbeg + 32 * (int64_t)c + (lane & 31) < end;
-      ChunkRegs r;
-      r.idx = ok ? cr.idx : zrow;
-      r.w = ok ? cr.r - cr.b : 0.f;
-      return r;
-    };
-    // Per iteration: gather half h+1 into F, run half h's MFMAs from P, then
-    // split F into P.  F is loaded and consumed inside one iteration and only
-    // VALU results (P) cross the back-edge, so no register copy there ever
-    // waits on a load in flight.
-    ChunkRaw h1 = ld32(1), h2 = ld32(2);
-    ChunkRaw h0 = ld32(0);
-    bias32(h0, 0);
-    bias32(h1, 1);
-    float F[8][NB], w[8];
-    u32x4_t P[3][NB];
-    gather_half<NB>(F, w, fin32(h0, 0), 0, Fc, row_bytes, q);
-    bf3_split<NB, USER>(P, cacc, sacc, wsum, F, w);
-    const int nhalves = (wlen + 31) >> 5;
-    for (int h = 0; h < nhalves; ++h) {
-      const ChunkRaw h3 = ld32(h + 3);
-      bias32(h2, h + 2);
-      gather_half<NB>(F, w, fin32(h1, h + 1), 0, Fc, row_bytes, q);
-      bf3_mfma<NB>(acc, P);
-      __builtin_amdgcn_sched_barrier(0);
-      bf3_split<NB, USER>(P, cacc, sacc, wsum, F, w);
-      h1 = h2;
-      h2 = h3;
+      cr.b = bias[ok ? cr.idx : zrow];
     }
+  };
+  auto fin32 = [&](const ChunkRaw& cr, int c) {
+    const bool ok = wbeg + 32 * (int64_t)c + (lane & 31) < end;
+    ChunkRegs r;
+    r.idx = ok ? cr.idx : zrow;
+    r.w = ok ? cr.r - cr.b : 0.f;
+    return r;
+  };
+  ChunkRaw h1 = ld32(1), h2 = ld32(2);
+  ChunkRaw h0 = ld32(0);
+  bias32(h0, 0);
+  bias32(h1, 1);
+  float Fr[8][NB], w[8];
+  u32x4_t P[3][NB];
+  gather_half<NB>(Fr, w, fin32(h0, 0), 0, Fc, row_bytes, q);
+  bf3_split<NB, USER>(P, cacc, sacc, wsum, Fr, w);
+  const int nhalves = (wlen + 31) >> 5;
+  for (int h = 0; h < nhalves; ++h) {
+    const ChunkRaw h3 = ld32(h + 3);
+    bias32(h2, h + 2);
+    gather_half<NB>(Fr, w, fin32(h1, h + 1), 0, Fc, row_bytes, q);
+    bf3_mfma<NB>(acc, P);
+    __builtin_amdgcn_sched_barrier(0);
+    bf3_split<NB, USER>(P, cacc, sacc, wsum, Fr, w);
+    h1 = h2;
+    h2 = h3;
   }
 
   // ---- epilogue -----------------------------------------------------------
@@ -927,22 +764,16 @@ __device__ __forceinline__ void gram_wave(
       if (USER) D.Gs[di * D.sV + c] = (c < k) ? sacc[b] : 0.f;
     }
   }
-  if (USER) {
-    const float wt = (__shfl(wsum, 0, 64) + __shfl(wsum, 16, 64)) +
-                     (__shfl(wsum, 32, 64) + __shfl(wsum, 48, 64));
-    if (lane == 0) {
-      D.Cb[di * D.sS] = wt;
-      D.Gn[di * D.sS] = (float)wlen;
-    }
+  const float wt = USER ? (__shfl(wsum, 0, 64) + __shfl(wsum, 16, 64)) +
+                              (__shfl(wsum, 32, 64) + __shfl(wsum, 48, 64))
+                        : 0.f;
+  if (USER && lane == 0) {
+    D.Cb[di * D.sS] = wt;
+    D.Gn[di * D.sS] = (float)wlen;
   }
   // tri16 layout (mr_internal.h): off-diagonal blocks as full tiles, diagonal
   // blocks folded pairwise; every store index is compile-time except the lane
   constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2, NTILE = NO + NF + (NB & 1);
-  auto st = [&](int off, float v) {
-    float* dst = &Gd[off];
-    if constexpr (NTS) __builtin_nontemporal_store(v, dst);
-    else *dst = v;
-  };
   int t = 0;
 #pragma unroll
   for (int bi = 0; bi < NB; ++bi) {
@@ -953,35 +784,31 @@ __device__ __forceinline__ void gram_wave(
         const int row = 4 * q + r;
         const float v = acc[t][r];
         if (bi != bj) {
-          st(off_index(bi, bj, NB) * 256 + row * 16 + col, v);
+          Gd[off_index(bi, bj, NB) * 256 + row * 16 + col] = v;
         } else if ((NB & 1) && bi == NB - 1) {
-          st((NO + NF) * 256 + row * 16 + col, v);
+          Gd[(NO + NF) * 256 + row * 16 + col] = v;
         } else if ((bi & 1) == 0) {
-          if (col >= row) st((NO + (bi >> 1)) * 256 + row * 16 + col, v);
+          if (col >= row) Gd[(NO + (bi >> 1)) * 256 + row * 16 + col] = v;
         } else {
-          if (col < row) st((NO + (bi >> 1)) * 256 + row * 16 + col, v);
-          else if (col == row) st(NTILE * 256 + (bi >> 1) * 16 + row, v);
+          if (col < row) Gd[(NO + (bi >> 1)) * 256 + row * 16 + col] = v;
+          else if (col == row) Gd[NTILE * 256 + (bi >> 1) * 16 + row] = v;
         }
       }
       ++t;
     }
   }
   if constexpr (FUSE) {
-    if (!to_slab) {
-      const float wt = USER ? (__shfl(wsum, 0, 64) + __shfl(wsum, 16, 64)) +
-                                  (__shfl(wsum, 32, 64) + __shfl(wsum, 48, 64))
-                            : 0.f;
+    if (!to_slab)
       start_from_acc<NB, USER>(acc, cacc, sacc, wt, (float)wlen, xv, xbv, went, k, ldk, cs,
                                *ssc, drr, dpq);
-    }
   }
 }
 
 // Waves are independent: one work item each, no block barriers -- except in
 // the FUSE form, whose waves then start the CG solve on their entity
-// (cg_start_entity; split entities are started after slab_reduce) and meet
+// (start_from_acc; split entities are started after slab_reduce) and meet
 // once at the end to store the block's (r.r, p.Gp) pair.
-template <int NB, int G, bool USER, bool NTS, bool FUSE>
+template <int NB, bool USER, bool FUSE>
 __global__ __launch_bounds__(256) void gram_kernel(
     const WorkItem* __restrict__ work, int64_t n_work,
     const int32_t* __restrict__ idx, const float* __restrict__ val,
@@ -992,13 +819,13 @@ __global__ __launch_bounds__(256) void gram_kernel(
   double drr = 0.0, dpq = 0.0;
   if constexpr (!FUSE) {
     if (wi >= n_work) return;
-    gram_wave<NB, G, USER, NTS, false>(wi, work, idx, val, F, bias, k, ldk, zrow, direct, slab,
-                                       cs, nullptr, drr, dpq);
+    gram_wave<NB, USER, false>(wi, work, idx, val, F, bias, k, ldk, zrow, direct, slab, cs,
+                               nullptr, drr, dpq);
   } else {
     __shared__ StartScratch<NB> scr[GRAM_WAVES];
     if (wi < n_work)
-      gram_wave<NB, G, USER, NTS, true>(wi, work, idx, val, F, bias, k, ldk, zrow, direct, slab,
-                                        cs, &scr[wid], drr, dpq);
+      gram_wave<NB, USER, true>(wi, work, idx, val, F, bias, k, ldk, zrow, direct, slab, cs,
+                                &scr[wid], drr, dpq);
     store_start_pair(drr, dpq, cs.parts);
   }
 }
@@ -1017,22 +844,17 @@ __global__ __launch_bounds__(256) void cg_start_split_kernel(const SplitItem* __
   store_start_pair(drr, dpq, parts);
 }
 
-template <int NB, int G>
-static int launch_gram_g(hipStream_t s, bool user_side, int k, const WorkItem* work,
-                         int64_t n_work, const int32_t* idx, const float* val,
-                         const float* F, const float* bias, int zrow, GramDst direct,
-                         GramDst slab, const CgStart* start) {
+template <int NB>
+static int launch_gram_nb(hipStream_t s, bool user_side, int k, const WorkItem* work,
+                          int64_t n_work, const int32_t* idx, const float* val,
+                          const float* F, const float* bias, int zrow, GramDst direct,
+                          GramDst slab, const CgStart* start) {
+  if (n_work <= 0) return 0;
   const int64_t grid = (n_work + GRAM_WAVES - 1) / GRAM_WAVES;
   const CgStart cs = start ? *start : CgStart{};
-  // MR_GRAM_LDS=bytes: extra dynamic LDS per block (caps blocks per CU; tuning)
-  static int lds = -1;
-  if (lds < 0) {
-    const char* e = getenv("MR_GRAM_LDS");
-    lds = e ? atoi(e) : 0;
-  }
-#define MR_GRAM_LAUNCH(U, FU)                                                     \
-  MR_LAUNCH((gram_kernel<NB, G, U, false, FU>), dim3((unsigned)grid), dim3(256), lds, s, \
-            work, n_work, idx, val, F, bias, k, ldk_of(k), zrow, direct, slab, cs)
+#define MR_GRAM_LAUNCH(U, FU)                                                           \
+  MR_LAUNCH((gram_kernel<NB, U, FU>), dim3((unsigned)grid), dim3(256), 0, s, work, n_work, \
+            idx, val, F, bias, k, ldk_of(k), zrow, direct, slab, cs)
   if (user_side) {
     if (start) MR_GRAM_LAUNCH(true, true); else MR_GRAM_LAUNCH(true, false);
   } else {
@@ -1041,31 +863,6 @@ static int launch_gram_g(hipStream_t s, bool user_side, int k, const WorkItem* w
 #undef MR_GRAM_LAUNCH
   MR_HIP(hipGetLastError());
   return 0;
-}
-
-// Pipeline group size G (steps of 4 ratings gathered per buffer).  Measured
-// on MI355X (tools/ab_variants.sh, ML-full shape, k = 64): G = 2 with 4
-// buffers is best (Gram 926 / 830 us vs 959 / 858 with G = 4, 2 buffers);
-// MR_GRAM_G=2|4|8 overrides (tuning).
-// Read per launch (a getenv), so tests can switch paths inside one process.
-static int gram_group_size(int nb) {
-  const char* e = getenv("MR_GRAM_G");
-  const char* b = getenv("MR_GRAM_BF3");
-  const int g = (b && atoi(b) == 0) ? (e ? atoi(e) : 2) : 0;
-  return (g == 0 || g == 2 || g == 4) ? g : 2;
-}
-
-template <int NB>
-static int launch_gram_nb(hipStream_t s, bool user_side, int k, const WorkItem* work,
-                          int64_t n_work, const int32_t* idx, const float* val,
-                          const float* F, const float* bias, int zrow, GramDst direct,
-                          GramDst slab, const CgStart* start) {
-  if (n_work <= 0) return 0;
-  switch (gram_group_size(NB)) {
-    case 0: return launch_gram_g<NB, 0>(s, user_side, k, work, n_work, idx, val, F, bias, zrow, direct, slab, start);
-    case 4: return launch_gram_g<NB, 4>(s, user_side, k, work, n_work, idx, val, F, bias, zrow, direct, slab, start);
-    default: return launch_gram_g<NB, 2>(s, user_side, k, work, n_work, idx, val, F, bias, zrow, direct, slab, start);
-  }
 }
 
 int launch_gram(hipStream_t s, bool user_side, int k, const WorkItem* work,
@@ -1235,8 +1032,12 @@ __device__ __forceinline__ void store_state(CgState* st, const CgScalars& v) {
   ast(&st->sharded, v.sharded);
 }
 
+// Seqlock publish into the host-mapped mirror (Engine::wait_mirror): odd
+// 2 seq - 1 marks a write in progress, the even 2 seq (release) its end.
 __device__ __forceinline__ void publish(const CgScalars& v, CgMirror* m, int seq) {
   if (!m) return;
+  __hip_atomic_store(&m->seq, 2 * seq - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __threadfence_system();
   m->done = v.done;
   m->fails = v.fails;
   m->it = v.it;
@@ -1245,7 +1046,7 @@ __device__ __forceinline__ void publish(const CgScalars& v, CgMirror* m, int seq
   m->rr = v.rr;
   m->final_rr = v.final_rr;
   __threadfence_system();
-  __hip_atomic_store(&m->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&m->seq, 2 * seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // INIT / ALPHA / BETA rules on the reduced sum s (one thread).
@@ -1327,13 +1128,17 @@ __device__ void last_block_finalize(CgState* st, int phase, double* partials, Cg
 }
 
 
-template <int NB, bool USER, bool NT>
+// G streams once per CG iteration and exceeds the Infinity Cache at scale,
+// so it is loaded non-temporally (measured on MI355X, k = 64, ML-full shape:
+// users 225 -> 195 us, items 103 -> 94 us, and the CG update 28 -> 25 us
+// because its vectors stay cached).
+template <int NB, bool USER>
 __global__ __launch_bounds__(256) void cg_matvec_kernel(
     const CgState* __restrict__ st, int update_p, int64_t E, int k, int ldk,
     const float* __restrict__ G, const float* __restrict__ Gs,
-    const float* __restrict__ Gn, float* __restrict__ v, float* __restrict__ vb,
-    const float* __restrict__ r, const float* __restrict__ rb,
-    float* __restrict__ y, float* __restrict__ yb, double* __restrict__ partials,
+    const float* __restrict__ Gn, double* __restrict__ v, double* __restrict__ vb,
+    const double* __restrict__ r, const double* __restrict__ rb,
+    double* __restrict__ y, double* __restrict__ yb, double* __restrict__ partials,
     CgState* fst, int phase) {
   if (ald(&st->done)) return;
   constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2, NTILE = NO + NF + (NB & 1);
@@ -1341,7 +1146,7 @@ __global__ __launch_bounds__(256) void cg_matvec_kernel(
   constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
   __shared__ MvScratch<NB> scr[MV_WAVES];
   __shared__ double sh[MV_WAVES];
-  const float beta = (float)ald(&st->beta);
+  const double beta = ald(&st->beta);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   MvScratch<NB>& sc = scr[wid];
   double dsum = 0.0;
@@ -1349,52 +1154,48 @@ __global__ __launch_bounds__(256) void cg_matvec_kernel(
        e += (int64_t)gridDim.x * MV_WAVES) {
     // issue order matters for the in-order vmcnt: vector loads first, then
     // every G block of this entity, so staging p waits only for the former
-    float* ve = v + e * ldk;
-    float vi[NV], ri[NV];
+    double* ve = v + e * ldk;
+    double vi[NV], ri[NV];
 #pragma unroll
     for (int h = 0; h < NV; ++h) {
       const int i = lane + 64 * h;
-      vi[h] = (i < NP) ? ve[i] : 0.f;                       // NP == ldk
-      ri[h] = (update_p && i < NP) ? r[e * ldk + i] : 0.f;
+      vi[h] = (i < NP) ? ve[i] : 0.0;                       // NP == ldk
+      ri[h] = (update_p && i < NP) ? r[e * ldk + i] : 0.0;
     }
-    float vbias = 0.f, rbias = 0.f;
+    double vbias = 0.0, rbias = 0.0;
     if (USER) {
       vbias = vb[e];
       if (update_p) rbias = rb[e];
     }
-    const float4* __restrict__ Ge = reinterpret_cast<const float4*>(G + e * GS);
+    const floatx4* __restrict__ Ge = reinterpret_cast<const floatx4*>(G + e * GS);
     float4 g[NTILE];
 #pragma unroll
     for (int t = 0; t < NTILE; ++t) {
-      if constexpr (NT) {
-        const floatx4 x = __builtin_nontemporal_load(
-            reinterpret_cast<const floatx4*>(Ge) + t * 64 + lane);
-        g[t] = make_float4(x[0], x[1], x[2], x[3]);
-      } else {
-        g[t] = Ge[t * 64 + lane];
-      }
+      const floatx4 x = __builtin_nontemporal_load(Ge + t * 64 + lane);
+      g[t] = make_float4(x[0], x[1], x[2], x[3]);
     }
     float d2 = 0.f;   // diagonal of the odd diagonal blocks (side array)
     if (NF > 0 && lane < 16 * NF) d2 = G[e * GS + NTILE * 256 + lane];
+    // p = -r + beta p (matrix.cpp:521) for the entity, then stage it
 #pragma unroll
     for (int h = 0; h < NV; ++h) {
       const int i = lane + 64 * h;
       if (i < NP) {
-        float x = vi[h];
+        double x = vi[h];
         if (update_p) {
-          x = fmaf(beta, x, -ri[h]);
+          x = fma(beta, x, -ri[h]);
           ve[i] = x;
         }
         sc.pv[virt_of(i, NB)] = x;
       }
     }
     if (USER && update_p) {
-      vbias = fmaf(beta, vbias, -rbias);
+      vbias = fma(beta, vbias, -rbias);
       if (lane == 0) vb[e] = vbias;
     }
     if (NF > 0 && lane < 16 * NF) sc.dd[lane] = d2;
     __builtin_amdgcn_wave_barrier();
-    float yo[NV], ybv = 0.f;
+    double yo[NV], ybv = 0.0;
     tile_matvec<NB, USER>(g, sc, vbias, USER ? Gs + e * ldk : nullptr, USER ? Gn[e] : 0.f, k,
                           yo, ybv);
     double d = 0.0;
@@ -1405,13 +1206,13 @@ __global__ __launch_bounds__(256) void cg_matvec_kernel(
         const int n = nat_of(o, NB);
         if (n < k) {
           y[e * ldk + n] = yo[h];
-          d += (double)yo[h] * sc.pv[o];
+          d = fma(yo[h], sc.pv[o], d);
         }
       }
     }
     if (USER && lane == 0) {
       yb[e] = ybv;
-      d += (double)ybv * vbias;
+      d = fma(ybv, vbias, d);
     }
     dsum += wave_sum_f64(d);
     __builtin_amdgcn_wave_barrier();
@@ -1422,116 +1223,105 @@ __global__ __launch_bounds__(256) void cg_matvec_kernel(
   if (fst && phase == CG_ALPHA) last_block_finalize(fst, CG_ALPHA, partials, nullptr, 0, sh);
 }
 
-// G streams once per CG iteration and exceeds the Infinity Cache at scale,
-// so it is loaded non-temporally: measured on MI355X (k = 64, ML-full shape)
-// users 225 -> 195 us, items 103 -> 94 us, and the CG update kernel 28 -> 25 us
-// because its vectors stay cached.  MR_MATVEC_NT=0 restores plain loads.
-static bool matvec_nt() {
-  static int env = -1;
-  if (env < 0) {
-    const char* e = getenv("MR_MATVEC_NT");
-    env = (e && atoi(e) == 0) ? 0 : 1;
-  }
-  return env == 1;
-}
-
-template <int NB>
-static int launch_matvec_nb(hipStream_t s, bool user_side, const CgState* st, int update_p,
-                            int64_t E, int k, const float* G, const float* Gs,
-                            const float* Gn, float* v, float* vb, const float* r,
-                            const float* rb, float* y, float* yb, double* partials,
-                            int n_part, CgState* fst, int phase) {
-  const bool nt = matvec_nt();
-#define MR_MV_LAUNCH(U, N)                                                          \
-  MR_LAUNCH((cg_matvec_kernel<NB, U, N>), dim3(n_part), dim3(256), 0, s,             \
-      st, update_p, E, k, ldk_of(k), G, Gs, Gn, v, vb, r, rb, y, yb, partials, fst, phase)
-  if (user_side) {
-    if (nt) MR_MV_LAUNCH(true, true); else MR_MV_LAUNCH(true, false);
-  } else {
-    if (nt) MR_MV_LAUNCH(false, true); else MR_MV_LAUNCH(false, false);
-  }
-#undef MR_MV_LAUNCH
-  MR_HIP(hipGetLastError());
-  return 0;
-}
-
 int launch_cg_matvec(hipStream_t s, bool user_side, const CgState* st,
                      int update_p, int64_t E, int k, const float* G,
-                     const float* Gs, const float* Gn, float* v, float* vb,
-                     const float* r, const float* rb, float* y, float* yb,
+                     const float* Gs, const float* Gn, double* v, double* vb,
+                     const double* r, const double* rb, double* y, double* yb,
                      double* partials, int n_part, CgState* fst, int phase) {
   if (n_part <= 0) return 0;
-#define MR_MV_CASE(NB)                                                               \
-  case NB:                                                                           \
-    return launch_matvec_nb<NB>(s, user_side, st, update_p, E, k, G, Gs, Gn, v, vb, r, \
-                                rb, y, yb, partials, n_part, fst, phase);
+#define MR_MV_CASE(NB)                                                                   \
+  case NB:                                                                               \
+    if (user_side)                                                                       \
+      MR_LAUNCH((cg_matvec_kernel<NB, true>), dim3(n_part), dim3(256), 0, s, st, update_p, \
+                E, k, ldk_of(k), G, Gs, Gn, v, vb, r, rb, y, yb, partials, fst, phase);   \
+    else                                                                                 \
+      MR_LAUNCH((cg_matvec_kernel<NB, false>), dim3(n_part), dim3(256), 0, s, st,         \
+                update_p, E, k, ldk_of(k), G, Gs, Gn, v, vb, r, rb, y, yb, partials, fst, \
+                phase);                                                                  \
+    break;
   switch (nb16_of(k)) {
     MR_MV_CASE(1) MR_MV_CASE(2) MR_MV_CASE(3) MR_MV_CASE(4)
     MR_MV_CASE(5) MR_MV_CASE(6) MR_MV_CASE(7) MR_MV_CASE(8)
     default: set_error("k > 128 not supported by the CG matvec"); return -1;
   }
 #undef MR_MV_CASE
+  MR_HIP(hipGetLastError());
+  return 0;
 }
 
 // ---------------------------------------------------------------------------
 // CG vector update (matrix.cpp:468-476 init, :501-507 step) + r.r partials.
-// Fixed grid, grid-stride, float4: reproducible partial sums.
+// x is the fp32 factor table, r / p / q are fp64; four elements per thread
+// and step.  Fixed grid, grid-stride: reproducible partial sums.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void cg_update_kernel(
     const CgState* __restrict__ st, int mode, int64_t n4, int64_t nb,
-    float* __restrict__ x, float* __restrict__ r, float* __restrict__ p,
-    const float* __restrict__ q, const float* __restrict__ c,
-    float* __restrict__ xb, float* __restrict__ rb, float* __restrict__ pb,
-    const float* __restrict__ qb, const float* __restrict__ cb,
+    float* __restrict__ x, double* __restrict__ r, double* __restrict__ p,
+    const double* __restrict__ q, const float* __restrict__ c,
+    float* __restrict__ xb, double* __restrict__ rb, double* __restrict__ pb,
+    const double* __restrict__ qb, const float* __restrict__ cb,
     double* __restrict__ partials, CgState* fst, CgMirror* mirror, int seq) {
   if (ald(&st->done)) return;
   __shared__ double sh[4];
   // sharded runs: alpha = rr / (all-reduced p.Ap), the ALPHA rule inline
-  const float alpha = (float)(ald(&st->sharded) && mode != UPD_INIT
-                                  ? ald(&st->rr) / ald(&st->comm[0])
-                                  : ald(&st->alpha));
+  const double alpha = ald(&st->sharded) && mode != UPD_INIT ? ald(&st->rr) / ald(&st->comm[0])
+                                                             : ald(&st->alpha);
   double acc = 0.0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  float4* r4 = reinterpret_cast<float4*>(r);
-  const float4* q4 = reinterpret_cast<const float4*>(q);
+  double2* r2 = reinterpret_cast<double2*>(r);
+  double2* p2 = reinterpret_cast<double2*>(p);
+  const double2* q2 = reinterpret_cast<const double2*>(q);
   if (mode == UPD_INIT) {
     const float4* c4 = reinterpret_cast<const float4*>(c);
-    float4* p4 = reinterpret_cast<float4*>(p);
     for (int64_t i = tid; i < n4; i += stride) {
-      const float4 a = q4[i], b = c4[i];
-      const float4 rr = make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
-      r4[i] = rr;
-      p4[i] = make_float4(-rr.x, -rr.y, -rr.z, -rr.w);
-      acc += (double)rr.x * rr.x + (double)rr.y * rr.y + (double)rr.z * rr.z +
-             (double)rr.w * rr.w;
+      const double2 qa = q2[2 * i], qb2 = q2[2 * i + 1];
+      const float4 cv = c4[i];
+      const double2 ra = make_double2(qa.x - (double)cv.x, qa.y - (double)cv.y);
+      const double2 rb2 = make_double2(qb2.x - (double)cv.z, qb2.y - (double)cv.w);
+      r2[2 * i] = ra;
+      r2[2 * i + 1] = rb2;
+      p2[2 * i] = make_double2(-ra.x, -ra.y);
+      p2[2 * i + 1] = make_double2(-rb2.x, -rb2.y);
+      acc = fma(ra.x, ra.x, acc);
+      acc = fma(ra.y, ra.y, acc);
+      acc = fma(rb2.x, rb2.x, acc);
+      acc = fma(rb2.y, rb2.y, acc);
     }
     for (int64_t i = tid; i < nb; i += stride) {
-      const float rr = qb[i] - cb[i];
-      rb[i] = rr;
-      pb[i] = -rr;
-      acc += (double)rr * rr;
+      const double rv = qb[i] - (double)cb[i];
+      rb[i] = rv;
+      pb[i] = -rv;
+      acc = fma(rv, rv, acc);
     }
   } else {
     float4* x4 = reinterpret_cast<float4*>(x);
-    const float4* p4 = reinterpret_cast<const float4*>(p);
     for (int64_t i = tid; i < n4; i += stride) {
-      float4 xv = x4[i], rv = r4[i];
-      const float4 pv = p4[i], qv = q4[i];
-      xv.x = fmaf(alpha, pv.x, xv.x); xv.y = fmaf(alpha, pv.y, xv.y);
-      xv.z = fmaf(alpha, pv.z, xv.z); xv.w = fmaf(alpha, pv.w, xv.w);
-      rv.x = fmaf(alpha, qv.x, rv.x); rv.y = fmaf(alpha, qv.y, rv.y);
-      rv.z = fmaf(alpha, qv.z, rv.z); rv.w = fmaf(alpha, qv.w, rv.w);
+      float4 xv = x4[i];
+      const double2 pa = p2[2 * i], pb2 = p2[2 * i + 1];
+      const double2 qa = q2[2 * i], qb2 = q2[2 * i + 1];
+      double2 ra = r2[2 * i], rb2 = r2[2 * i + 1];
+      xv.x = (float)fma(alpha, pa.x, (double)xv.x);
+      xv.y = (float)fma(alpha, pa.y, (double)xv.y);
+      xv.z = (float)fma(alpha, pb2.x, (double)xv.z);
+      xv.w = (float)fma(alpha, pb2.y, (double)xv.w);
+      ra.x = fma(alpha, qa.x, ra.x);
+      ra.y = fma(alpha, qa.y, ra.y);
+      rb2.x = fma(alpha, qb2.x, rb2.x);
+      rb2.y = fma(alpha, qb2.y, rb2.y);
       x4[i] = xv;
-      r4[i] = rv;
-      acc += (double)rv.x * rv.x + (double)rv.y * rv.y + (double)rv.z * rv.z +
-             (double)rv.w * rv.w;
+      r2[2 * i] = ra;
+      r2[2 * i + 1] = rb2;
+      acc = fma(ra.x, ra.x, acc);
+      acc = fma(ra.y, ra.y, acc);
+      acc = fma(rb2.x, rb2.x, acc);
+      acc = fma(rb2.y, rb2.y, acc);
     }
     for (int64_t i = tid; i < nb; i += stride) {
-      xb[i] = fmaf(alpha, pb[i], xb[i]);
-      const float rv = fmaf(alpha, qb[i], rb[i]);
+      xb[i] = (float)fma(alpha, pb[i], (double)xb[i]);
+      const double rv = fma(alpha, qb[i], rb[i]);
       rb[i] = rv;
-      acc += (double)rv * rv;
+      acc = fma(rv, rv, acc);
     }
   }
   const double tot = block_sum_f64<256>(acc, sh);
@@ -1542,14 +1332,26 @@ __global__ __launch_bounds__(256) void cg_update_kernel(
 }
 
 int launch_cg_update(hipStream_t s, const CgState* st, int mode, int64_t n,
-                     int64_t nb, float* x, float* r, float* p, const float* q,
-                     const float* c, float* xb, float* rb, float* pb,
-                     const float* qb, const float* cb, double* partials,
+                     int64_t nb, float* x, double* r, double* p, const double* q,
+                     const float* c, float* xb, double* rb, double* pb,
+                     const double* qb, const float* cb, double* partials,
                      int n_part, CgState* fst, CgMirror* mirror, int seq) {
   MR_LAUNCH(cg_update_kernel, dim3(n_part), dim3(256), 0, s,
       st, mode, n / 4, nb, x, r, p, q, c, xb, rb, pb, qb, cb, partials, fst, mirror, seq);
   MR_HIP(hipGetLastError());
   return 0;
+}
+
+// Unfused CG start: v = x (fp32 factor rows, + bias) as fp64, so the matvec
+// can form G x.
+__global__ void x_to_vec_kernel(int64_t n, int64_t nb, const float* __restrict__ x,
+                                const float* __restrict__ xb, double* __restrict__ v,
+                                double* __restrict__ vb) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    v[t] = x[t];
+    if (t < nb) vb[t] = xb[t];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1810,6 +1612,14 @@ __global__ void predict_kernel(int64_t n, int k, int ldk, const int* __restrict_
     for (int j = 0; j < k; ++j) s += (double)Uf[u * ldk + j] * Vf[i * ldk + j];
     out[t] = s + Ub[u];
   }
+}
+
+int launch_x_to_vec(hipStream_t s, int64_t n, int64_t nb, const float* x, const float* xb,
+                    double* v, double* vb) {
+  if (n <= 0) return 0;
+  x_to_vec_kernel<<<grid_for(n), 256, 0, s>>>(n, nb, x, xb, v, vb);
+  MR_HIP(hipGetLastError());
+  return 0;
 }
 
 int launch_predict(hipStream_t s, int64_t n, int k, int ldk, const int* uid,

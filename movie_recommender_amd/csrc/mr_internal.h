@@ -65,9 +65,13 @@ __host__ __device__ inline int ldk_of(int k) { return (k + 15) & ~15; }
 //   * the NB(NB-1)/2 strictly-upper blocks (bi < bj) as full tiles, row-major
 //     inside, row-major upper order;
 //   * the diagonal blocks folded in pairs (2m, 2m+1) into ONE tile F_m:
-//     F_m[r][c] = D_2m[r][c] for c >= r, D_2m+1[r][c] for c < r (each D is
-//     bitwise symmetric, so no transpose is ever needed), and the diagonal of
-//     D_2m+1 in a 16-float side array; an odd last diagonal block stays full.
+//     F_m[r][c] = D_2m[r][c] for c >= r, D_2m+1[r][c] for c < r, and the
+//     diagonal of D_2m+1 in a 16-float side array; an odd last diagonal
+//     block is stored full but only its upper triangle is G.  The bf16x3 MFMA
+//     sums are NOT bitwise symmetric (B[i][j] and B[j][i] add the hm / mh
+//     products in opposite orders), so every reader -- GEMV, fused CG start,
+//     Cholesky, read-back -- takes each diagonal entry pair from the one
+//     stored triangle: G is exactly symmetric.
 // k = 64: 8 tiles + 32 floats = 2,080 floats = k(k+1)/2 (full: 4,096).
 // Rows/cols >= k are zero.
 __host__ __device__ inline int nb16_of(int k) { return (k + 15) / 16; }
@@ -140,7 +144,7 @@ struct GramDst {
 struct CgStart {
   const float* x;    // this side's iterate (local rows), ldk stride
   const float* xb;   // user side: bias column of the iterate
-  float *r, *rb, *p, *pb, *q, *qb;
+  double *r, *rb, *p, *pb, *q, *qb;   // fp64 CG vectors
   double* parts;
 };
 
@@ -195,13 +199,6 @@ int launch_gram(hipStream_t s, bool user_side, int k, const WorkItem* work,
 inline int64_t gram_blocks(int64_t n_work) { return (n_work + 3) / 4; }
 int launch_cg_start_split(hipStream_t s, bool user_side, int k, const SplitItem* split,
                           int64_t n_split, GramDst direct, const CgStart& cs, double* parts);
-// bf16x3 normal equations (gram3.hip): Fs = launch_split_table(F) once per
-// half-step, rows x 3 parts x ldk bf16 in virtual column order.
-bool gram3_supported(int k);
-int launch_split_table(hipStream_t s, int64_t rows, int k, const float* F, uint16_t* Fs);
-int launch_gram3(hipStream_t s, bool user_side, int k, const WorkItem* work, int64_t n_work,
-                 const int32_t* idx, const float* val, const uint16_t* Fs, const float* bias,
-                 int zrow, GramDst direct, GramDst slab);
 int launch_slab_reduce(hipStream_t s, bool user_side, int k,
                        const SplitItem* split, int64_t n_split,
                        const float* slab, int64_t rec, GramDst direct);
@@ -210,16 +207,20 @@ int launch_slab_reduce(hipStream_t s, bool user_side, int k,
 // apply the INIT / BETA rules and publish to `mirror` -- no control kernels.
 int launch_cg_matvec(hipStream_t s, bool user_side, const CgState* st,
                      int update_p, int64_t E, int k, const float* G,
-                     const float* Gs, const float* Gn, float* v, float* vb,
-                     const float* r, const float* rb, float* y, float* yb,
+                     const float* Gs, const float* Gn, double* v, double* vb,
+                     const double* r, const double* rb, double* y, double* yb,
                      double* partials, int n_part, CgState* fst = nullptr,
                      int phase = CG_INIT);
+// x is the fp32 factor table (and bias), r / p / q the fp64 CG vectors.
 int launch_cg_update(hipStream_t s, const CgState* st, int mode, int64_t n,
-                     int64_t nb, float* x, float* r, float* p, const float* q,
-                     const float* c, float* xb, float* rb, float* pb,
-                     const float* qb, const float* cb, double* partials,
+                     int64_t nb, float* x, double* r, double* p, const double* q,
+                     const float* c, float* xb, double* rb, double* pb,
+                     const double* qb, const float* cb, double* partials,
                      int n_part, CgState* fst = nullptr, CgMirror* mirror = nullptr,
                      int seq = 0);
+// v[0..n) = x, vb[0..nb) = xb as fp64 (unfused CG start).
+int launch_x_to_vec(hipStream_t s, int64_t n, int64_t nb, const float* x, const float* xb,
+                    double* v, double* vb);
 // phase CG_START: partials are n_part (r.r, p.Gp) pairs; min_dec / max_it /
 // sharded initialise the state.
 int launch_cg_control(hipStream_t s, CgState* st, int phase, int ctl,

@@ -12,6 +12,7 @@ import numpy as np
 from . import _lib
 
 SOLVERS = {"cg": 0, "cholesky": 1}
+OPTIONS = {"fuse_start": 0, "cg_speculate": 1, "wait_timeout_s": 2}   # include/mr_als.h
 
 
 def _i32(a):
@@ -92,6 +93,12 @@ class AlsContext:
         _lib.check(_lib.lib().mr_als_set_solver(self._h, SOLVERS[solver], float(ridge)),
                    "mr_als_set_solver")
 
+    def set_option(self, name, value):
+        """Engine option (``mr_als_set_option``): ``fuse_start``,
+        ``cg_speculate`` (0/1) or ``wait_timeout_s``."""
+        _lib.check(_lib.lib().mr_als_set_option(self._h, OPTIONS[name], float(value)),
+                   "mr_als_set_option")
+
     def set_timing(self, enable=True):
         _lib.check(_lib.lib().mr_als_set_timing(self._h, int(bool(enable))),
                    "mr_als_set_timing")
@@ -132,10 +139,20 @@ class AlsContext:
         """Exactly ``n`` ALS iterations (user + item half-step each)."""
         _lib.check(_lib.lib().mr_als_iterate(self._h, int(n)), "mr_als_iterate")
 
-    def half_step(self, side):
+    def half_step(self, side, min_r_decrease=None, max_iteration=None):
+        """One half-step; returns (CG iterations, final rr).  Default CG
+        arguments are the reference's (0.01, 200); others go through
+        ``mr_als_half_step_ex``."""
         rr = ctypes.c_double(0)
-        its = _lib.check(_lib.lib().mr_als_half_step(
-            self._h, 0 if side in (0, "users") else 1, ctypes.byref(rr)), "mr_als_half_step")
+        sd = 0 if side in (0, "users") else 1
+        if min_r_decrease is None and max_iteration is None:
+            its = _lib.check(_lib.lib().mr_als_half_step(self._h, sd, ctypes.byref(rr)),
+                             "mr_als_half_step")
+        else:
+            its = _lib.check(_lib.lib().mr_als_half_step_ex(
+                self._h, sd, 0.01 if min_r_decrease is None else float(min_r_decrease),
+                200 if max_iteration is None else int(max_iteration), ctypes.byref(rr)),
+                "mr_als_half_step_ex")
         return its, rr.value
 
     def build_normal_equations(self, side):
@@ -153,6 +170,16 @@ class AlsContext:
             self._h, 0 if user else 1, len(ents), ents.ctypes.data_as(_lib.IP),
             G.ctypes.data_as(_lib.DP), c.ctypes.data_as(_lib.DP)), "mr_als_get_normal_equations")
         return G, c
+
+    def cg_vectors(self, side):
+        """(r, p, q) of the side's last CG solve, fp64 (users: k+1 per user)."""
+        user = side in (0, "users")
+        n = (self.num_users * (self.k + 1)) if user else (self.num_items * self.k)
+        out = [np.empty(n) for _ in range(3)]
+        _lib.check(_lib.lib().mr_als_get_cg_vectors(
+            self._h, 0 if user else 1, *[a.ctypes.data_as(_lib.DP) for a in out]),
+            "mr_als_get_cg_vectors")
+        return tuple(out)
 
     def sync(self):
         _lib.check(_lib.lib().mr_als_sync(self._h), "mr_als_sync")

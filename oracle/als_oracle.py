@@ -10,7 +10,11 @@ Two equivalent forms are provided:
   ``(k+1)^2`` block per user and ``k^2`` per item, so the CG matvec is a
   batched per-entity GEMV ``G_e p_e``.  Same CG scalars, same stop rules.
   This is the form the HIP path implements; ``dtype=np.float32`` emulates
-  its precision (fp32 Gram and vectors, fp64 dot products and scalars).
+  its precision: fp32 normal equations (G, c) and factor tables (x), fp64
+  CG vectors r / p / q with every product G p accumulated in fp64, fp64 dot
+  products and scalars.  (fp32 r / p / q drift by percents from the
+  reference on ill-conditioned blocks -- the 60 x 50, k = 32 fixture -- and
+  are not used.)
 
 Plus the exact per-entity solve (``als_exact``; Cholesky mode) and the
 reference's ``als_predict``.
@@ -223,20 +227,20 @@ def block_matvec(G):
     """``(G x)_e = G_e x_e`` on the concatenated vector."""
     E, K, _ = G.shape
 
+    Gd = G.astype(np.float64)   # fp32 entries, fp64 products and sums
+
     def mv(x):
-        xe = x.reshape(E, K)
-        if G.dtype == np.float32:
-            y = np.einsum("eij,ej->ei", G.astype(np.float64), xe.astype(np.float64))
-            return y.astype(np.float32).reshape(-1)
-        return np.einsum("eij,ej->ei", G, xe).reshape(-1)
+        xe = np.asarray(x, np.float64).reshape(E, K)
+        return np.einsum("eij,ej->ei", Gd, xe).reshape(-1)
     return mv
 
 
 def cg_blocks(G, c, x, min_r_decrease=0.01, max_iteration=200):
-    """Block-Gram CG: ``cg_normal`` with the batched block GEMV."""
-    vdtype = np.float32 if G.dtype == np.float32 else np.float64
-    return cg_normal(block_matvec(G), c.reshape(-1).astype(vdtype), x,
-                     min_r_decrease, max_iteration, vdtype=vdtype)
+    """Block-Gram CG: ``cg_normal`` with the batched block GEMV.  Vectors are
+    fp64; ``x`` keeps its own dtype (fp32 factor tables: x += alpha p is
+    formed in fp64 and rounded)."""
+    return cg_normal(block_matvec(G), np.asarray(c, np.float64).reshape(-1), x,
+                     min_r_decrease, max_iteration)
 
 
 def als_block(user_ids, item_ids, ratings, k, U0, V0,

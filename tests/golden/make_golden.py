@@ -206,9 +206,58 @@ def g4():
     print("G4 test rmse", tr.min(), tr.max(), "train", trn.min(), trn.max())
 
 
+def g6():
+    """Headline-k fixtures (round 2): the k = 64 / 128 CG path (NB = 4 / 8
+    block GEMV, fused CG start) pinned to the reference, plus the dense
+    60 x 50, k = 32 case on which fp32 CG vectors drifted by 3 %.
+
+    Dense: all users rate all items, 80 % kept (cpp_ls_test.test_als shape).
+    ML-shaped: power-law degrees with a minimum degree of ~2k, so the reference
+    is thread-count invariant (tc_spread recorded; realistic ill-conditioned
+    data is covered by the G4 band)."""
+    cases = [("als_dense_60x50_k32_it3.npz", (60, 50, 32, 1, 3, 3)),
+             ("als_dense_300x260_k64.npz", (300, 260, 64, 7, 3, 200)),
+             ("als_dense_400x300_k128.npz", (400, 300, 128, 7, 3, 200))]
+    for name, (nu, ni, k, dseed, iseed, mi) in cases:
+        u, i, r, tu, ti, tr = synth.dense_fixture(nu, ni, k, 0.8, seed=dseed)
+        U0, V0 = ref.init_factors(nu, ni, k, iseed)
+        res = {}
+        for tc in (8, 1):
+            ref.set_thread_count(tc)
+            res[tc] = ref.als(u, i, r, k, U0, V0, max_iteration=mi)
+        U, V, ret = res[8]
+        spread = max(np.max(np.abs(res[1][0] - U)) / np.max(np.abs(U)),
+                     np.max(np.abs(res[1][1] - V)) / np.max(np.abs(V)))
+        np.savez_compressed(os.path.join(HERE, name), user_ids=u, item_ids=i, ratings=r,
+                            k=k, num_users=nu, num_items=ni, max_iteration=mi,
+                            U0=U0, V0=V0, U=U, V=V, ret=ret, ret_tc1=res[1][2],
+                            tc_spread=spread, meta=json.dumps(_meta(8)))
+        print("G6", name, "N", len(r), "ret", ret, "tc1 ret", res[1][2], "spread", spread,
+              flush=True)
+    k = 64
+    rs_ = synth.movielens_like((4000, 1500, 900_000), 2 * k, seed=synth.DATA_SEED)
+    U0, V0 = ref.init_factors(rs_.num_users, rs_.num_items, k, 5)
+    for n_it in (2, 4):
+        res = {}
+        for tc in (8, 1):
+            ref.set_thread_count(tc)
+            res[tc] = ref.als(rs_.user_ids, rs_.item_ids, rs_.ratings, k, U0, V0,
+                              max_iteration=n_it)
+        U, V, ret = res[8]
+        spread = max(np.max(np.abs(res[1][0] - U)) / np.max(np.abs(U)),
+                     np.max(np.abs(res[1][1] - V)) / np.max(np.abs(V)))
+        name = f"als_mlshape_k{k}_it{n_it}.npz"
+        np.savez_compressed(os.path.join(HERE, name), user_ids=rs_.user_ids,
+                            item_ids=rs_.item_ids, ratings=rs_.ratings, k=k,
+                            num_users=rs_.num_users, num_items=rs_.num_items,
+                            min_degree=2 * k, U0=U0, V0=V0, U=U, V=V, ret=ret,
+                            tc_spread=spread, meta=json.dumps(_meta(8)))
+        print("G6", name, "N", rs_.n, "U", rs_.num_users, "I", rs_.num_items, "ret", ret,
+              "tc spread", spread, flush=True)
+    ref.set_thread_count(1)
+
+
 if __name__ == "__main__":
-    g1()
-    g2()
-    g3()
-    g4()
-    g5()
+    steps = sys.argv[1:] or ["g1", "g2", "g3", "g4", "g5", "g6"]
+    for s in steps:
+        globals()[s]()

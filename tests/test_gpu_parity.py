@@ -1,10 +1,12 @@
 """GPU parity: the HIP path (through the C ABI) against the compiled
 reference's golden vectors and the CPU oracle.
 
-Tolerances (fp32 normal equations and CG vectors, fp64 CG scalars):
-  * dense golden fixtures (G2):  max|x - ref| / max|ref| <= 1e-5, same `ret`
-  * MovieLens-shaped sparse fixtures (G3, 60-100 CG iterations per
-    half-step, fp32 round-off accumulates): <= 5e-5, same `ret`
+Tolerances (fp32 normal equations, fp64 CG vectors r / p / q and scalars,
+products G p accumulated in fp64; north_star: "within 1e-5 relative"):
+  * dense golden fixtures (G2, k = 3 .. 128):  max|x - ref| / max|ref| <= 1e-5,
+    same `ret`
+  * MovieLens-shaped sparse fixtures (G3, k = 10, 32, 64; 40-100 CG iterations
+    per half-step): <= 1e-5, same `ret`
   * general CG least squares (fp64 on the GPU): <= 1e-9, same iterations
   * Gram kernel vs fp64 NumPy Gram on sampled entities: <= 2e-5 relative to
     the block's largest entry
@@ -21,9 +23,30 @@ from conftest import GOLDEN, load_golden, rel_err
 pytestmark = pytest.mark.gpu
 
 DENSE = ["als_dense_38x45_k5.npz", "als_dense_40x45_k3.npz",
-         "als_dense_300x200_k10.npz", "als_dense_200x150_k32.npz"]
+         "als_dense_300x200_k10.npz", "als_dense_200x150_k32.npz",
+         "als_dense_60x50_k32_it3.npz", "als_dense_300x260_k64.npz",
+         "als_dense_400x300_k128.npz"]
 MLSHAPE = ["als_mlshape_k10_it2.npz", "als_mlshape_k10_it4.npz",
-           "als_mlshape_k32_it2.npz", "als_mlshape_k32_it4.npz"]
+           "als_mlshape_k32_it2.npz", "als_mlshape_k32_it4.npz",
+           "als_mlshape_k64_it2.npz", "als_mlshape_k64_it4.npz"]
+# headline-k fixtures: NB = 4 / 8 block GEMV and the fused CG start
+HEADLINE = ["als_dense_60x50_k32_it3.npz", "als_dense_300x260_k64.npz",
+            "als_dense_400x300_k128.npz", "als_mlshape_k64_it4.npz"]
+
+
+def max_iteration_of(name, d):
+    if "max_iteration" in d:
+        return int(d["max_iteration"])
+    if "_it" in name:
+        return int(name.split("_it")[1].split(".")[0])
+    return 200
+
+
+def tolerance_of(d):
+    """1e-5 (north_star), or twice the reference's own thread-count spread on
+    a fixture where that is larger (the ill-conditioned 60 x 50, k = 32 case:
+    6.2e-4 between 1 and 8 threads)."""
+    return max(1e-5, 2 * float(d["tc_spread"]))
 
 
 def abi_als(L, d, max_iteration=200, min_r_decrease=0.01):
@@ -47,20 +70,57 @@ def abi_als(L, d, max_iteration=200, min_r_decrease=0.01):
 @pytest.mark.parametrize("name", DENSE)
 def test_als_dense_golden(gpu, name):
     d = load_golden(name)
-    U, V, ret = abi_als(gpu, d)
+    U, V, ret = abi_als(gpu, d, max_iteration=max_iteration_of(name, d))
     assert ret == int(d["ret"])
-    assert rel_err(U, d["U"]) <= 1e-5, rel_err(U, d["U"])
-    assert rel_err(V, d["V"]) <= 1e-5, rel_err(V, d["V"])
+    tol = tolerance_of(d)
+    assert rel_err(U, d["U"]) <= tol, rel_err(U, d["U"])
+    assert rel_err(V, d["V"]) <= tol, rel_err(V, d["V"])
 
 
 @pytest.mark.parametrize("name", MLSHAPE)
 def test_als_mlshape_golden(gpu, name):
     d = load_golden(name)
-    n_it = int(name.split("_it")[1].split(".")[0])
-    U, V, ret = abi_als(gpu, d, max_iteration=n_it)
+    U, V, ret = abi_als(gpu, d, max_iteration=max_iteration_of(name, d))
     assert ret == int(d["ret"])
-    assert rel_err(U, d["U"]) <= 5e-5, rel_err(U, d["U"])
-    assert rel_err(V, d["V"]) <= 5e-5, rel_err(V, d["V"])
+    tol = tolerance_of(d)
+    assert rel_err(U, d["U"]) <= tol, rel_err(U, d["U"])
+    assert rel_err(V, d["V"]) <= tol, rel_err(V, d["V"])
+
+
+@pytest.mark.parametrize("name", HEADLINE)
+@pytest.mark.parametrize("chunk,fuse", [(2048, 1), (64, 1), (2048, 0)])
+def test_headline_paths_golden(gpu, name, chunk, fuse):
+    """Every CG start path against the compiled reference at k = 32 / 64 /
+    128: the Gram-epilogue start (fuse 1), the start of split entities after
+    slab_reduce (chunk 64 splits every entity), and the unfused reference
+    order (fuse 0: x -> matvec -> INIT update).  Speculative launches on and
+    off must give identical CG counts and bitwise-identical factors."""
+    from movie_recommender_amd.engine import AlsContext
+    from movie_recommender_amd import _lib
+    d = load_golden(name)
+    k, nU, nI = int(d["k"]), int(d["num_users"]), int(d["num_items"])
+    mi = max_iteration_of(name, d)
+    outs = []
+    try:
+        for spec in (1, 0):
+            with AlsContext(d["user_ids"], d["item_ids"], d["ratings"], k, nU, nI,
+                            gram_chunk=chunk) as ctx:
+                ctx.set_option("fuse_start", fuse)
+                ctx.set_option("cg_speculate", spec)
+                ctx.set_factors(d["U0"], d["V0"])
+                ret = ctx.run(0.01, mi)
+                st = ctx.stats()
+                outs.append((ctx.get_factors(), ret, st["cg_users_total"], st["cg_items_total"]))
+    finally:
+        _lib.check(_lib.lib().mr_set_gram_chunk(2048), "reset chunk")
+    (U, V), ret, cu, ci = outs[0]
+    assert ret == int(d["ret"])
+    tol = tolerance_of(d)
+    assert rel_err(U, d["U"]) <= tol, rel_err(U, d["U"])
+    assert rel_err(V, d["V"]) <= tol, rel_err(V, d["V"])
+    (U2, V2), ret2, cu2, ci2 = outs[1]
+    assert (ret2, cu2, ci2) == (ret, cu, ci)
+    assert np.array_equal(U, U2) and np.array_equal(V, V2)
 
 
 def test_cg_least_squares_golden(gpu):
@@ -164,17 +224,11 @@ def test_replay_from_snapshot_is_bitwise_identical(gpu):
         assert np.array_equal(U, U1) and np.array_equal(V, V1)
 
 
-@pytest.mark.parametrize("k,path", [(3, "bf3"), (10, "bf3"), (16, "bf3"), (32, "bf3"),
-                                    (33, "bf3"), (64, "bf3"), (65, "bf3"), (96, "bf3"),
-                                    (128, "bf3"), (10, "f32"), (33, "f32"), (64, "f32"),
-                                    (128, "f32"), (20, "gram3"), (64, "gram3")])
-def test_gram_kernel_vs_numpy(gpu, k, path, monkeypatch):
-    """Normal equations of both sides against fp64 NumPy, including heavy
-    entities split across waves (chunk 64 forces slabs) and empty entities.
-    Paths: bf3 = default in-register bf16x3 split on the bf16 MFMA; f32 = the
-    fp32 MFMA loop (MR_GRAM_BF3=0); gram3 = pre-split table (MR_GRAM3=1)."""
-    monkeypatch.setenv("MR_GRAM3", "1" if path == "gram3" else "0")
-    monkeypatch.setenv("MR_GRAM_BF3", "0" if path == "f32" else "1")
+@pytest.mark.parametrize("k", [3, 10, 16, 20, 32, 33, 64, 65, 96, 128])
+def test_gram_kernel_vs_numpy(gpu, k):
+    """Normal equations of both sides (bf16x3 split on the bf16 MFMA) against
+    fp64 NumPy, including heavy entities split across waves (chunk 64 forces
+    slabs) and empty entities."""
     from movie_recommender_amd.engine import AlsContext
     from oracle import als_oracle as O
     rng = np.random.default_rng(k)
@@ -202,6 +256,60 @@ def test_gram_kernel_vs_numpy(gpu, k, path, monkeypatch):
             assert np.all(G[-1] == 0) and np.all(c[-1] == 0)   # empty entity
     from movie_recommender_amd import _lib
     _lib.check(_lib.lib().mr_set_gram_chunk(2048), "reset chunk")
+
+
+@pytest.mark.parametrize("k", [5, 10, 32, 33, 64, 65, 128])
+@pytest.mark.parametrize("fuse,chunk", [(1, 2048), (1, 64), (0, 2048)])
+def test_cg_iterations_vs_oracle(gpu, k, fuse, chunk):
+    """The first CG iterations of both sides -- CG start (fused in the Gram
+    epilogue, after slab_reduce for split entities, or the unfused matvec +
+    INIT update), the NB = 1..8 block GEMV, the update and the fused control
+    -- against the oracle's fp64 CG (matrix.cpp:456-529 in block form) run on
+    the GPU's own normal equations (fp32 values read back).  What remains is
+    summation order: final rr within 1e-10, x within 2 fp32 ulps."""
+    from movie_recommender_amd.engine import AlsContext
+    from movie_recommender_amd import _lib
+    from oracle import als_oracle as O
+    rng = np.random.default_rng(100 + k)
+    nU, nI = 90, 70
+    n = 6000
+    u = rng.integers(0, nU - 2, n).astype(np.int32)       # last 2 users: no ratings
+    i = (rng.zipf(1.3, n) % (nI - 1)).astype(np.int32)    # heavy items, last item empty
+    key = np.unique(u.astype(np.int64) * nI + i)
+    u = (key // nI).astype(np.int32)
+    i = (key % nI).astype(np.int32)
+    r = rng.normal(0, 1, len(u))
+    U0 = rng.uniform(-1, 1, nU * (k + 1)).astype(np.float32).astype(np.float64)
+    V0 = rng.uniform(-1, 1, nI * k).astype(np.float32).astype(np.float64)
+    try:
+        with AlsContext(u, i, r, k, nU, nI, gram_chunk=chunk) as ctx:
+            ctx.set_option("fuse_start", fuse)
+            for side, nE in (("users", nU), ("items", nI)):
+                ctx.set_factors(U0, V0)
+                ctx.build_normal_equations(side)
+                G, c = ctx.normal_equations(side, np.arange(nE))
+                x0 = (U0 if side == "users" else V0).astype(np.float32)
+                r0 = np.einsum("eij,ej->ei", G, x0.astype(np.float64).reshape(nE, -1)).ravel() \
+                    - c.ravel()
+                for m in (0, 1, 2, 4):
+                    ctx.set_factors(U0, V0)
+                    its, rr = ctx.half_step(side, 0.01, m)
+                    U, V = ctx.get_factors()
+                    if m == 0:   # r0 = G x - c, p0 = -r0 (matrix.cpp:468-476)
+                        rv, pv, _ = ctx.cg_vectors(side)
+                        sc = np.max(np.abs(r0))
+                        assert np.max(np.abs(rv - r0)) <= 1e-13 * sc, np.max(np.abs(rv - r0)) / sc
+                        assert np.array_equal(pv, -rv)
+                    x = x0.copy()
+                    ito, rro = O.cg_blocks(G, c, x, 0.01, m)
+                    got = U if side == "users" else V
+                    assert its == ito, (side, m, its, ito)
+                    assert abs(rr - rro) <= 1e-10 * abs(rro), (side, m, rr, rro)
+                    step = np.max(np.abs(x.astype(np.float64) - x0))
+                    assert np.max(np.abs(got - x)) <= 1e-9 * step + 2 * np.spacing(np.float32(1)), \
+                        (side, m, np.max(np.abs(got - x)), step)
+    finally:
+        _lib.check(_lib.lib().mr_set_gram_chunk(2048), "reset chunk")
 
 
 def test_split_vs_unsplit_same_result(gpu):

@@ -13,9 +13,22 @@ from conftest import GOLDEN, load_golden, rel_err
 from oracle import als_oracle as O
 
 DENSE = ["als_dense_38x45_k5.npz", "als_dense_40x45_k3.npz",
-         "als_dense_300x200_k10.npz", "als_dense_200x150_k32.npz"]
+         "als_dense_300x200_k10.npz", "als_dense_200x150_k32.npz",
+         "als_dense_60x50_k32_it3.npz"]
 MLSHAPE = ["als_mlshape_k10_it2.npz", "als_mlshape_k10_it4.npz",
            "als_mlshape_k32_it2.npz", "als_mlshape_k32_it4.npz"]
+# headline k (64 / 128): block form and the GPU precision only (the
+# design-matrix restatement is too slow for these in the CPU suite)
+HEADLINE = ["als_dense_300x260_k64.npz", "als_dense_400x300_k128.npz",
+            "als_mlshape_k64_it2.npz", "als_mlshape_k64_it4.npz"]
+
+
+def max_iteration_of(name, d):
+    if "max_iteration" in d:
+        return int(d["max_iteration"])
+    if "_it" in name:
+        return int(name.split("_it")[1].split(".")[0])
+    return 200
 
 
 def test_cg_golden():
@@ -33,33 +46,52 @@ def test_cg_golden():
 def test_als_design_form_golden(name):
     d = load_golden(name)
     k = int(d["k"])
-    U, V, ret, _ = O.als_design(d["user_ids"], d["item_ids"], d["ratings"], k, d["U0"], d["V0"])
+    U, V, ret, _ = O.als_design(d["user_ids"], d["item_ids"], d["ratings"], k, d["U0"], d["V0"],
+                                max_iteration=max_iteration_of(name, d))
     assert ret == int(d["ret"])
-    assert rel_err(U, d["U"]) < 1e-12 and rel_err(V, d["V"]) < 1e-12
+    tol = max(1e-12, 20 * float(d["tc_spread"]))
+    assert rel_err(U, d["U"]) < tol and rel_err(V, d["V"]) < tol
 
 
-@pytest.mark.parametrize("name", DENSE + MLSHAPE)
+@pytest.mark.parametrize("name", DENSE + MLSHAPE + HEADLINE)
 def test_als_block_form_golden(name):
     """The block-Gram form (what the HIP path computes) equals the reference."""
     d = load_golden(name)
     k = int(d["k"])
-    max_it = 200 if name.startswith("als_dense") else int(name.split("_it")[1].split(".")[0])
     U, V, ret, _ = O.als_block(d["user_ids"], d["item_ids"], d["ratings"], k, d["U0"], d["V0"],
-                               max_iteration=max_it)
+                               max_iteration=max_iteration_of(name, d))
     assert ret == int(d["ret"])
     tol = max(1e-10, 20 * float(d["tc_spread"]))
     assert rel_err(U, d["U"]) < tol and rel_err(V, d["V"]) < tol
 
 
-@pytest.mark.parametrize("name", DENSE[:3])
-def test_als_block_fp32_within_tolerance(name):
-    """fp32 Gram/vectors + fp64 scalars stays within 1e-5 of the reference."""
+@pytest.mark.parametrize("name", DENSE + MLSHAPE + HEADLINE)
+def test_als_block_gpu_precision_within_tolerance(name):
+    """The HIP path's precision (fp32 G, c and factors; fp64 CG vectors and
+    products) stays within 1e-5 of the reference with the same `ret`; on the
+    ill-conditioned 60 x 50, k = 32 fixture the reference itself moves by
+    6e-4 between thread counts, so there the bound is its own spread."""
     d = load_golden(name)
     k = int(d["k"])
     U, V, ret, _ = O.als_block(d["user_ids"], d["item_ids"], d["ratings"], k, d["U0"], d["V0"],
-                               dtype=np.float32)
+                               max_iteration=max_iteration_of(name, d), dtype=np.float32)
     assert ret == int(d["ret"])
-    assert rel_err(U, d["U"]) < 1e-5 and rel_err(V, d["V"]) < 1e-5
+    tol = max(1e-5, 2 * float(d["tc_spread"]))
+    assert rel_err(U, d["U"]) < tol and rel_err(V, d["V"]) < tol, (rel_err(U, d["U"]),
+                                                                  rel_err(V, d["V"]))
+
+
+def test_gpu_precision_tracks_fp64_on_ill_conditioned_case():
+    """60 x 50, k = 32 (40 ratings for 33 unknowns per user): the HIP path's
+    precision follows the fp64 block form to 1e-5 with identical CG counts
+    (fp32 CG vectors drift 2.7 % / 3.1 % with CG counts 168 / 156 vs 155 / 141)."""
+    d = load_golden("als_dense_60x50_k32_it3.npz")
+    args = (d["user_ids"], d["item_ids"], d["ratings"], 32, d["U0"], d["V0"])
+    U64, V64, r64, t64 = O.als_block(*args, max_iteration=3)
+    U32, V32, r32, t32 = O.als_block(*args, max_iteration=3, dtype=np.float32)
+    assert r32 == r64
+    assert [t[:2] for t in t32] == [t[:2] for t in t64]
+    assert rel_err(U32, U64) < 1e-5 and rel_err(V32, V64) < 1e-5
 
 
 def test_reference_statistical_check_on_golden():
