@@ -99,6 +99,18 @@ def algorithmic_cost(cls, k, n_users, n_items, n_ratings, ldk, fused=True):
     return 0, 0
 
 
+def iteration_roofline(k, rate):
+    """SURVEY.md 8(d) whole-iteration roofline at R ratings/s: algorithmic
+    bytes B(k) = 20 + 8k per rating (two (idx, value) reads, one k-float row
+    gather per side) and flops F(k) = 2(k+1)^2 + 2k^2 + 2(k+1) + 2k (full Gram
+    outer products + rhs, both sides), as fractions of the HBM and FP32 peaks."""
+    B = 20 + 8 * k
+    F = 2 * (k + 1) ** 2 + 2 * k ** 2 + 2 * (k + 1) + 2 * k
+    return {"bytes_per_rating": B, "flops_per_rating": F,
+            "hbm_GBps": round(B * rate / 1e9, 1), "hbm_frac": round(B * rate / 8e12, 4),
+            "fp32_TFps": round(F * rate / 1e12, 2), "fp32_frac": round(F * rate / 157.3e12, 4)}
+
+
 def cpu_baseline(shape, k, threads, scale, seed=0):
     """Reference CPU path on a bounded sample of the same workload: the
     MovieLens-shaped generator at ``scale`` of the users, items and draws (so
@@ -145,7 +157,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--force-shard", action="store_true",
                     help="use the sharded RCCL path even with one rank (testing)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r01.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r02.json"),
                     help="per-kernel HBM bytes from a rocprofv3 --pmc run (optional)")
     args = ap.parse_args()
 
@@ -296,7 +308,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32+f64",
         "data": "synthetic (MovieLens-full shape, seeded; no MovieLens data offline)",
         "config": {"workload": f"ALS iteration, {args.shape} shape, k={k}, solver={args.solver}",
                    "k": k, "n_ratings": int(rs.n), "users": int(rs.num_users),
@@ -307,6 +319,7 @@ def main():
                      "traffic": traffic,
                      "alg_bytes_per_launch": int(nbytes), "alg_flops_per_launch": int(nflops),
                      "avg_launch_us": round(avg_s * 1e6, 2), "gather": gather},
+        "iteration_roofline": iteration_roofline(k, value),
         "cg_iterations": {"users_total": st["cg_users_total"],
                           "items_total": st["cg_items_total"],
                           "per_step_users": st["cg_users_total"] / args.steps,

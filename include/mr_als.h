@@ -162,6 +162,14 @@ int mr_als_get_normal_equations(mr_als* ctx, int side, int n, const int* entitie
  * entry last, k per item) of the side's last solve; any may be NULL.  Tests. */
 int mr_als_get_cg_vectors(mr_als* ctx, int side, double* r, double* p, double* q);
 
+/* The side's device CSR (off[E+1], idx[nnz] = other side's id, val[nnz] as
+ * fp32) and its Gram work list (n = mr_als_work_items entries, heavy first:
+ * rating range [begin, begin+len) of local entity `entity`, slab >= 0 for a
+ * chunk of a split entity).  Any pointer may be NULL.  Tests. */
+long long mr_als_work_items(mr_als* ctx, int side);
+int mr_als_get_layout(mr_als* ctx, int side, long long* off, int* idx, float* val,
+                      long long* wbegin, int* wlen, int* went, int* wslab);
+
 int mr_als_get_stats(mr_als* ctx, mr_stats* out);
 int mr_als_reset_stats(mr_als* ctx);
 /* Waits for all work queued on the context's stream. */

@@ -286,6 +286,20 @@ int mr_als_get_cg_vectors(mr_als* ctx, int side, double* r, double* p, double* q
   return guarded([&]() { return ctx->eng.get_cg_vectors(side == MR_SIDE_USERS, r, p, q); });
 }
 
+long long mr_als_work_items(mr_als* ctx, int side) {
+  if (!ctx) return -1;
+  return side == MR_SIDE_USERS ? ctx->eng.su.n_work : ctx->eng.si.n_work;
+}
+
+int mr_als_get_layout(mr_als* ctx, int side, long long* off, int* idx, float* val,
+                      long long* wbegin, int* wlen, int* went, int* wslab) {
+  MR_CHECK(ctx, "null context");
+  MR_CHECK(side == MR_SIDE_USERS || side == MR_SIDE_ITEMS, "unknown side");
+  return guarded([&]() {
+    return ctx->eng.get_layout(side == MR_SIDE_USERS, off, idx, val, wbegin, wlen, went, wslab);
+  });
+}
+
 int mr_als_get_normal_equations(mr_als* ctx, int side, int n, const int* entities,
                                 double* G_out, double* c_out) {
   MR_CHECK(ctx, "null context");

@@ -78,15 +78,15 @@ int build_csr(hipStream_t s, int64_t n, int64_t E, const int32_t* d_key,
   size_t tb = 0;
   int rc = -1;
   do {
-    if (hipMallocAsync((void**)&k0, n * 4, s) != hipSuccess) break;
-    if (hipMallocAsync((void**)&k1, n * 4, s) != hipSuccess) break;
-    if (hipMallocAsync((void**)&v0, n * 4, s) != hipSuccess) break;
-    if (hipMallocAsync((void**)&v1, n * 4, s) != hipSuccess) break;
+    if (hipMalloc((void**)&k0, n * 4) != hipSuccess) break;
+    if (hipMalloc((void**)&k1, n * 4) != hipSuccess) break;
+    if (hipMalloc((void**)&v0, n * 4) != hipSuccess) break;
+    if (hipMalloc((void**)&v1, n * 4) != hipSuccess) break;
     shift_keys_kernel<<<grid_of(n), 256, 0, s>>>(n, d_key, key_base, k0);
     iota_kernel<<<grid_of(n), 256, 0, s>>>(n, v0);
     if (rocprim::radix_sort_pairs(nullptr, tb, k0, k1, v0, v1, (size_t)n, 0, bits, s) !=
         hipSuccess) break;
-    if (hipMallocAsync(&tmp, tb, s) != hipSuccess) break;
+    if (hipMalloc(&tmp, tb) != hipSuccess) break;
     if (rocprim::radix_sort_pairs(tmp, tb, k0, k1, v0, v1, (size_t)n, 0, bits, s) !=
         hipSuccess) break;
     gather_kernel<TV, TIn><<<grid_of(n), 256, 0, s>>>(n, v1, d_other, d_val, idx, val);
@@ -94,11 +94,13 @@ int build_csr(hipStream_t s, int64_t n, int64_t E, const int32_t* d_key,
     if (hipGetLastError() != hipSuccess) break;
     rc = 0;
   } while (0);
-  if (tmp) (void)hipFreeAsync(tmp, s);
-  if (k0) (void)hipFreeAsync(k0, s);
-  if (k1) (void)hipFreeAsync(k1, s);
-  if (v0) (void)hipFreeAsync(v0, s);
-  if (v1) (void)hipFreeAsync(v1, s);
+  // temporaries from hipMalloc, not the stream-ordered pool (engine.hip dalloc)
+  (void)hipStreamSynchronize(s);
+  if (tmp) (void)hipFree(tmp);
+  if (k0) (void)hipFree(k0);
+  if (k1) (void)hipFree(k1);
+  if (v0) (void)hipFree(v0);
+  if (v1) (void)hipFree(v1);
   if (rc != 0) set_error("build_csr: device sort failed (out of memory?)");
   return rc;
 }

@@ -118,6 +118,8 @@ struct Engine {
   int predict(int64_t n, const int* uid, const int* iid, double* out);
   int get_normal_equations(bool user, int n, const int* ents, double* G, double* c);
   int get_cg_vectors(bool user, double* r, double* p, double* q);
+  int get_layout(bool user, long long* off, int* idx, float* val, long long* wbegin,
+                 int* wlen, int* went, int* wslab);
   // timing
   int ev_get(hipEvent_t* e);
   int tic(int cls, int tag, hipEvent_t* a);

@@ -32,16 +32,27 @@ void set_error(const std::string& msg) {
 }
 const char* last_error() { return g_err.c_str(); }
 
+// Device buffers come from hipMalloc, never from the stream-ordered pool
+// (hipMallocAsync): on this ROCm (7.2, gfx950) a hipMemcpyAsync into a pool
+// buffer can overtake a kernel still reading that buffer on the same stream,
+// and a D2H copy out of one can return data older than the kernel that wrote
+// it -- pinned or pageable host side alike; the same copies on hipMalloc
+// buffers stay ordered (tools/probes/xfer_order.hip, profiles/r02/xfer_order.txt).
+// That was the root cause of round 1's stale set -> get round trips.
 template <typename T>
 static int dalloc(T** p, int64_t n, hipStream_t s) {
+  (void)s;
   *p = nullptr;
   if (n <= 0) n = 1;
-  MR_HIP(hipMallocAsync((void**)p, (size_t)n * sizeof(T), s));
+  MR_HIP(hipMalloc((void**)p, (size_t)n * sizeof(T)));
   return 0;
 }
 template <typename T>
 static void dfree(T*& p, hipStream_t s) {
-  if (p) (void)hipFreeAsync(p, s);
+  if (p) {
+    (void)hipStreamSynchronize(s);
+    (void)hipFree(p);
+  }
   p = nullptr;
 }
 
@@ -164,7 +175,7 @@ int Engine::build_side(Side& S, bool user, int64_t n, const int32_t* d_key,
     return -1;
   // host copy of the offsets -> work list (chunks, heavy first)
   std::vector<int64_t> off(S.E + 1);
-  MR_HIP(hipMemcpyAsync(off.data(), S.off, (S.E + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+  MR_D2H(off.data(), S.off, (S.E + 1) * sizeof(int64_t), stream);
   MR_HIP(hipStreamSynchronize(stream));
   std::vector<WorkItem> work;
   std::vector<SplitItem> split;
@@ -195,9 +206,9 @@ int Engine::build_side(Side& S, bool user, int64_t n, const int32_t* d_key,
       dalloc(&S.slab, S.n_slab * S.rec, stream))
     return -1;
   if (S.n_work)
-    MR_HIP(hipMemcpyAsync(S.work, work.data(), S.n_work * sizeof(WorkItem), hipMemcpyHostToDevice, stream));
+    MR_H2D(S.work, work.data(), S.n_work * sizeof(WorkItem), stream);
   if (S.n_split)
-    MR_HIP(hipMemcpyAsync(S.split, split.data(), S.n_split * sizeof(SplitItem), hipMemcpyHostToDevice, stream));
+    MR_H2D(S.split, split.data(), S.n_split * sizeof(SplitItem), stream);
   // normal equations + CG vectors
   const int64_t ef = S.E * ldk;
   if (dalloc(&S.G, S.E * gsize_of(k), stream) || dalloc(&S.C, ef, stream) ||
@@ -275,9 +286,9 @@ int Engine::init(int dev, int k_, int64_t U_, int64_t I_, int64_t n_u,
     double* dr = nullptr;
     if (dalloc(&du, n, stream) || dalloc(&di, n, stream) || dalloc(&dr, n, stream)) return -1;
     if (n > 0) {
-      MR_HIP(hipMemcpyAsync(du, hu, n * 4, hipMemcpyHostToDevice, stream));
-      MR_HIP(hipMemcpyAsync(di, hi, n * 4, hipMemcpyHostToDevice, stream));
-      MR_HIP(hipMemcpyAsync(dr, hr, n * 8, hipMemcpyHostToDevice, stream));
+      MR_H2D(du, hu, n * 4, stream);
+      MR_H2D(di, hi, n * 4, stream);
+      MR_H2D(dr, hr, n * 8, stream);
     }
     // id range validation (the reference has none: out-of-range ids are UB)
     MR_HIP(hipMemsetAsync(d_flag, 0, 16, stream));
@@ -288,7 +299,7 @@ int Engine::init(int dev, int k_, int64_t U_, int64_t I_, int64_t n_u,
                             view == 1 || same ? (int32_t)i1 : (int32_t)I, d_flag + 1))
       return -1;
     int flags[2] = {0, 0};
-    MR_HIP(hipMemcpyAsync(flags, d_flag, 8, hipMemcpyDeviceToHost, stream));
+    MR_D2H(flags, d_flag, 8, stream);
     MR_HIP(hipStreamSynchronize(stream));
     if (view == 0 && !same) {
       MR_CHECK(!flags[0], "user view: user id outside this shard's user range");
@@ -427,9 +438,9 @@ int Engine::allgather_side(bool user) {
   const int64_t rowf = user ? ldk + 1 : ldk;
   std::vector<float> tab(rows * rowf);
   std::vector<float> fac(rows * ldk), bias(user ? rows : 0);
-  MR_HIP(hipMemcpyAsync(fac.data(), user ? Ufac : Vfac, rows * ldk * 4, hipMemcpyDeviceToHost, stream));
+  MR_D2H(fac.data(), user ? Ufac : Vfac, rows * ldk * 4, stream);
   if (user)
-    MR_HIP(hipMemcpyAsync(bias.data(), Ubias, rows * 4, hipMemcpyDeviceToHost, stream));
+    MR_D2H(bias.data(), Ubias, rows * 4, stream);
   MR_HIP(hipStreamSynchronize(stream));
   for (int64_t r = 0; r < rows; ++r) {
     memcpy(&tab[r * rowf], &fac[r * ldk], ldk * 4);
@@ -441,9 +452,9 @@ int Engine::allgather_side(bool user) {
     memcpy(&fac[r * ldk], &tab[r * rowf], ldk * 4);
     if (user) bias[r] = tab[r * rowf + ldk];
   }
-  MR_HIP(hipMemcpyAsync(user ? Ufac : Vfac, fac.data(), rows * ldk * 4, hipMemcpyHostToDevice, stream));
+  MR_H2D(user ? Ufac : Vfac, fac.data(), rows * ldk * 4, stream);
   if (user)
-    MR_HIP(hipMemcpyAsync(Ubias, bias.data(), rows * 4, hipMemcpyHostToDevice, stream));
+    MR_H2D(Ubias, bias.data(), rows * 4, stream);
   MR_HIP(hipStreamSynchronize(stream));
   return 0;
 }
@@ -704,7 +715,7 @@ int Engine::solve(Side& S) {
     return -1;
   if (toc(MR_K_SOLVE, -1, a)) return -1;
   int bad = 0;
-  MR_HIP(hipMemcpyAsync(&bad, d_flag, 4, hipMemcpyDeviceToHost, stream));
+  MR_D2H(&bad, d_flag, 4, stream);
   MR_HIP(hipStreamSynchronize(stream));
   if (S.user) stats.nonpd_users += bad;
   else stats.nonpd_items += bad;
@@ -785,17 +796,17 @@ int Engine::predict(int64_t n, const int* uid, const int* iid, double* out) {
   double* dout = nullptr;
   if (dalloc(&du, n, stream) || dalloc(&di, n, stream) || dalloc(&dout, n, stream)) return -1;
   if (n > 0) {
-    MR_HIP(hipMemcpyAsync(du, uid, n * 4, hipMemcpyHostToDevice, stream));
-    MR_HIP(hipMemcpyAsync(di, iid, n * 4, hipMemcpyHostToDevice, stream));
+    MR_H2D(du, uid, n * 4, stream);
+    MR_H2D(di, iid, n * 4, stream);
     MR_HIP(hipMemsetAsync(d_flag, 0, 8, stream));
     if (launch_validate_ids(stream, n, du, 0, (int32_t)U, d_flag)) return -1;
     if (launch_validate_ids(stream, n, di, 0, (int32_t)I, d_flag + 1)) return -1;
     int flags[2];
-    MR_HIP(hipMemcpyAsync(flags, d_flag, 8, hipMemcpyDeviceToHost, stream));
+    MR_D2H(flags, d_flag, 8, stream);
     MR_HIP(hipStreamSynchronize(stream));
     MR_CHECK(!flags[0] && !flags[1], "predict: id out of range");
     if (launch_predict(stream, n, k, ldk, du, di, Ufac, Ubias, Vfac, dout)) return -1;
-    MR_HIP(hipMemcpyAsync(out, dout, n * 8, hipMemcpyDeviceToHost, stream));
+    MR_D2H(out, dout, n * 8, stream);
   }
   MR_HIP(hipStreamSynchronize(stream));
   dfree(du, stream); dfree(di, stream); dfree(dout, stream);
@@ -812,12 +823,12 @@ int Engine::get_normal_equations(bool user, int n, const int* ents, double* G, d
   for (int t = 0; t < n; ++t) {
     const int64_t e = ents[t];
     MR_CHECK(e >= 0 && e < S.E, "entity out of range");
-    MR_HIP(hipMemcpyAsync(g.data(), S.G + e * gsize_of(k), gsize_of(k) * 4, hipMemcpyDeviceToHost, stream));
-    MR_HIP(hipMemcpyAsync(v.data(), S.C + e * ldk, ldk * 4, hipMemcpyDeviceToHost, stream));
+    MR_D2H(g.data(), S.G + e * gsize_of(k), gsize_of(k) * 4, stream);
+    MR_D2H(v.data(), S.C + e * ldk, ldk * 4, stream);
     if (user) {
-      MR_HIP(hipMemcpyAsync(s.data(), S.Gs + e * ldk, ldk * 4, hipMemcpyDeviceToHost, stream));
-      MR_HIP(hipMemcpyAsync(&cb, S.Cb + e, 4, hipMemcpyDeviceToHost, stream));
-      MR_HIP(hipMemcpyAsync(&gn, S.Gn + e, 4, hipMemcpyDeviceToHost, stream));
+      MR_D2H(s.data(), S.Gs + e * ldk, ldk * 4, stream);
+      MR_D2H(&cb, S.Cb + e, 4, stream);
+      MR_D2H(&gn, S.Gn + e, 4, stream);
     }
     MR_HIP(hipStreamSynchronize(stream));
     double* Ge = G + (size_t)t * K * K;
@@ -838,6 +849,33 @@ int Engine::get_normal_equations(bool user, int n, const int* ents, double* G, d
   return 0;
 }
 
+// The side's device CSR and Gram work list, for tests (a full-size check that
+// the context build -- uploads, device sort, offsets, work list -- landed
+// exactly).  Any pointer may be NULL.
+int Engine::get_layout(bool user, long long* off, int* idx, float* val, long long* wbegin,
+                       int* wlen, int* went, int* wslab) {
+  MR_HIP(hipSetDevice(device));
+  Side& S = user ? su : si;
+  if (off) {
+    std::vector<int64_t> o(S.E + 1);
+    MR_D2H(o.data(), S.off, o.size() * 8, stream);
+    for (int64_t e = 0; e <= S.E; ++e) off[e] = o[e];
+  }
+  if (idx) MR_D2H(idx, S.idx, S.nnz * 4, stream);
+  if (val) MR_D2H(val, S.val, S.nnz * 4, stream);
+  if (wbegin || wlen || went || wslab) {
+    std::vector<WorkItem> w(S.n_work);
+    MR_D2H(w.data(), S.work, w.size() * sizeof(WorkItem), stream);
+    for (int64_t t = 0; t < S.n_work; ++t) {
+      if (wbegin) wbegin[t] = w[t].begin;
+      if (wlen) wlen[t] = w[t].len;
+      if (went) went[t] = w[t].entity;
+      if (wslab) wslab[t] = w[t].slab;
+    }
+  }
+  return 0;
+}
+
 // CG vectors r, p, q of the side as left by the last solve (K = k+1 per user
 // with the bias entry last, k per item), for tests.
 int Engine::get_cg_vectors(bool user, double* r, double* p, double* q) {
@@ -850,8 +888,8 @@ int Engine::get_cg_vectors(bool user, double* r, double* p, double* q) {
   double* bvs[3] = {S.rb, S.pb, S.qb};
   for (int t = 0; t < 3; ++t) {
     if (!outs[t]) continue;
-    MR_HIP(hipMemcpyAsync(v.data(), vecs[t], v.size() * 8, hipMemcpyDeviceToHost, stream));
-    if (user) MR_HIP(hipMemcpyAsync(b.data(), bvs[t], b.size() * 8, hipMemcpyDeviceToHost, stream));
+    MR_D2H(v.data(), vecs[t], v.size() * 8, stream);
+    if (user) MR_D2H(b.data(), bvs[t], b.size() * 8, stream);
     MR_HIP(hipStreamSynchronize(stream));
     for (int64_t e = 0; e < S.E; ++e) {
       for (int j = 0; j < k; ++j) outs[t][e * K + j] = v[e * ldk + j];
@@ -880,13 +918,14 @@ int cg_ls_f64(int device, int rows, int cols, const int* rp, const int* ci,
     hipStream_t s;
     std::vector<void*> p;
     ~Bufs() {
-      for (void* q : p) (void)hipFreeAsync(q, s);
+      (void)hipStreamSynchronize(s);
+      for (void* q : p) (void)hipFree(q);
       (void)hipStreamSynchronize(s);
       (void)hipStreamDestroy(s);
     }
   } bufs{s, {}};
   auto alloc = [&](void** q, size_t bytes) -> int {
-    MR_HIP(hipMallocAsync(q, bytes ? bytes : 8, s));
+    MR_HIP(hipMalloc(q, bytes ? bytes : 8));   // not the stream-ordered pool (dalloc)
     bufs.p.push_back(*q);
     return 0;
   };
@@ -906,13 +945,13 @@ int cg_ls_f64(int device, int rows, int cols, const int* rp, const int* ci,
     return -1;
   MR_HIP(hipHostMalloc((void**)&h_st, sizeof(CgState), hipHostMallocDefault));
   struct HFree { CgState* h; ~HFree() { (void)hipHostFree(h); } } hf{h_st};
-  MR_HIP(hipMemcpyAsync(d_rp32, rp, (rows + 1) * 4, hipMemcpyHostToDevice, s));
+  MR_H2D(d_rp32, rp, (rows + 1) * 4, s);
   if (nnz) {
-    MR_HIP(hipMemcpyAsync(d_ci, ci, nnz * 4, hipMemcpyHostToDevice, s));
-    MR_HIP(hipMemcpyAsync(d_v, v, nnz * 8, hipMemcpyHostToDevice, s));
+    MR_H2D(d_ci, ci, nnz * 4, s);
+    MR_H2D(d_v, v, nnz * 8, s);
   }
-  if (rows) MR_HIP(hipMemcpyAsync(d_b, b, (int64_t)rows * 8, hipMemcpyHostToDevice, s));
-  if (cols) MR_HIP(hipMemcpyAsync(d_x, x, (int64_t)cols * 8, hipMemcpyHostToDevice, s));
+  if (rows) MR_H2D(d_b, b, (int64_t)rows * 8, s);
+  if (cols) MR_H2D(d_x, x, (int64_t)cols * 8, s);
   if (launch_i32_to_i64(s, rows + 1, d_rp32, d_rp)) return -1;
   // explicit transpose on the device (sparse_matrix_transpose, matrix.cpp:617-692)
   if (launch_rows_of(s, rows, d_rp, d_rowof)) return -1;
@@ -949,7 +988,7 @@ int cg_ls_f64(int device, int rows, int cols, const int* rp, const int* ci,
     MR_CHECK(t <= max_it + 64, "CG did not terminate");
     chunk_it = std::min(chunk_it * 2, 16);
   }
-  if (cols) MR_HIP(hipMemcpyAsync(x, d_x, (int64_t)cols * 8, hipMemcpyDeviceToHost, s));
+  if (cols) MR_D2H(x, d_x, (int64_t)cols * 8, s);
   MR_HIP(hipStreamSynchronize(s));
   if (final_rr) *final_rr = h_st->final_rr;
   return h_st->ret;

@@ -354,75 +354,77 @@ struct StartScratch {
   float sGs[16 * NB];                // user side: row sums, virtual order
 };
 
+// Accumulator tile of upper block (bi, bj), bi <= bj, row-major upper order.
+__host__ __device__ constexpr int acc_tile(int bi, int bj, int nb) {
+  return bi * nb - bi * (bi - 1) / 2 + (bj - bi);
+}
+
 // y = G v straight from the MFMA accumulators of the Gram wave (no memory
 // round trip), products accumulated in fp64.  acc[t(bi,bj)] (bi <= bj,
 // diagonal blocks FULL) holds B[4q + r][col] in lane (q, col).  Row products
 // B v_bj go to y_bi (summed over the 16 lanes of row q by DPP), column
 // products B^T v_bi to y_bj (summed over the 4 rows by lane shuffles), both
-// in a fixed order; a diagonal block contributes its stored triangle only.  v in sc.pv (virtual order).
-// Returns y at virtual o = lane + 64 h in yo[h] (without the bias column) --
-// 0 for padding.
+// in a fixed order; a diagonal block contributes its stored triangle only.
+// Two passes (block rows, then block columns) with one tile's fp64 copy live
+// at a time: this epilogue must fit the main loop's register budget (3 waves
+// per SIMD at k = 64), so tile conversions are not hoisted
+// (sched_barrier).  v in sc.pv (virtual order).  Returns y at virtual
+// o = lane + 64 h in yo[h] (without the bias column) -- 0 for padding.
 template <int NB>
 __device__ __forceinline__ void acc_matvec(const floatx4 (&acc)[NB * (NB + 1) / 2],
                                            StartScratch<NB>& sc, int k,
                                            double (&yo)[(16 * NB + 63) / 64]) {
   constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
   const int lane = threadIdx.x & 63, q = lane >> 4, col = lane & 15;
-  double R[NB][4], Cp[NB];
-#pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    Cp[b] = 0.0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) R[b][r] = 0.0;
-  }
-  int t = 0;
+  // pass 1: row products y_bi[4q + r] = sum_bj B(bi,bj)[4q + r][:] v_bj
 #pragma unroll
   for (int bi = 0; bi < NB; ++bi) {
-    const double2 va = *reinterpret_cast<const double2*>(&sc.pv[16 * bi + 4 * q]);
-    const double2 vb = *reinterpret_cast<const double2*>(&sc.pv[16 * bi + 4 * q + 2]);
+    const bool lower = (bi & 1) && !((NB & 1) && bi == NB - 1);
+    double R[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int bj = bi; bj < NB; ++bj) {
+      const int t = acc_tile(bi, bj, NB);
       const double vj = sc.pv[16 * bj + col];
-      const double a[4] = {acc[t][0], acc[t][1], acc[t][2], acc[t][3]};
-      const double vr[4] = {va.x, va.y, vb.x, vb.y};   // v_bi at rows 4q + r
-      if (bi != bj) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) R[bi][r] = fma(a[r], vj, R[bi][r]);
-        double c = Cp[bj];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) c = fma(a[r], vr[r], c);
-        Cp[bj] = c;
-      } else {
+      for (int r = 0; r < 4; ++r) {
+        const int row = 4 * q + r;
         // diagonal block: the bf16x3 sum is not bitwise symmetric, so use
         // exactly the triangle tri16 stores (upper for even blocks and the
-        // odd last block, lower + side diagonal for odd folded blocks) for
-        // both the row and the transposed product, as the GEMV does
-        const bool lower = (bi & 1) && !((NB & 1) && bi == NB - 1);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = 4 * q + r;
-          const bool rowuse = lower ? (col <= row) : (col >= row);
-          const bool coluse = lower ? (col < row) : (col > row);
-          R[bi][r] = fma(rowuse ? a[r] : 0.0, vj, R[bi][r]);
-          Cp[bi] = fma(coluse ? a[r] : 0.0, vr[r], Cp[bi]);
-        }
+        // odd last block, lower + side diagonal for odd folded blocks)
+        const bool use = bi != bj || (lower ? (col <= row) : (col >= row));
+        R[r] = fma(use ? (double)acc[t][r] : 0.0, vj, R[r]);
       }
-      ++t;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double rs = row_sum_f64(R[r]);
+      // lanes 0..3 of row q hold identical row sums: lane (q, r) stores row 4q + r
+      if (col == r) sc.yR[16 * bi + 4 * q + r] = rs;
     }
   }
+  // pass 2: column products y_bj[col] = sum_{bi <= bj} B(bi,bj)[:][col] . v_bi
 #pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    double rs[4];
+  for (int bj = 0; bj < NB; ++bj) {
+    const bool lower = (bj & 1) && !((NB & 1) && bj == NB - 1);
+    double c = 0.0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) rs[r] = row_sum_f64(R[b][r]);
-    // lanes 0..3 of row q hold identical row sums: lane (q, r) stores row 4q + r
+    for (int bi = 0; bi <= bj; ++bi) {
+      const int t = acc_tile(bi, bj, NB);
+      const double2 va = *reinterpret_cast<const double2*>(&sc.pv[16 * bi + 4 * q]);
+      const double2 vb = *reinterpret_cast<const double2*>(&sc.pv[16 * bi + 4 * q + 2]);
+      const double vr[4] = {va.x, va.y, vb.x, vb.y};   // v_bi at rows 4q + r
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (col == r) sc.yR[16 * b + 4 * q + r] = rs[r];
-    double c = Cp[b];
+      for (int r = 0; r < 4; ++r) {
+        const int row = 4 * q + r;
+        const bool use = bi != bj || (lower ? (col < row) : (col > row));
+        c = fma(use ? (double)acc[t][r] : 0.0, vr[r], c);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
     c += __shfl_xor(c, 16, 64);
     c += __shfl_xor(c, 32, 64);   // identical in all 4 rows
-    if (q == 0) sc.yC[16 * b + col] = c;
+    if (q == 0) sc.yC[16 * bj + col] = c;
   }
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -809,7 +811,7 @@ __device__ __forceinline__ void gram_wave(
 // (start_from_acc; split entities are started after slab_reduce) and meet
 // once at the end to store the block's (r.r, p.Gp) pair.
 template <int NB, bool USER, bool FUSE>
-__global__ __launch_bounds__(256) void gram_kernel(
+__global__ __launch_bounds__(256, (NB <= 4 ? 3 : 1)) void gram_kernel(
     const WorkItem* __restrict__ work, int64_t n_work,
     const int32_t* __restrict__ idx, const float* __restrict__ val,
     const float* __restrict__ F, const float* __restrict__ bias, int k, int ldk, int zrow,

@@ -54,6 +54,28 @@ const char* last_error();
     }                                                                         \
   } while (0)
 
+// Host <-> device copies through two pinned chunks (xfer.hip), stream-ordered
+// on s; both return with their copies complete.  Caller buffers are never
+// handed to the DMA engine as pageable memory.
+struct Stager {
+  static constexpr size_t kChunk = size_t(16) << 20;
+  void* buf[2] = {nullptr, nullptr};
+  ~Stager();
+  int init();
+  int h2d(hipStream_t s, void* dst, const void* src, size_t bytes);
+  int d2h(hipStream_t s, void* dst, const void* src, size_t bytes);
+};
+extern thread_local Stager t_stager;
+
+#define MR_H2D(dst, src, bytes, s)                                         \
+  do {                                                                     \
+    if (::mr::t_stager.h2d((s), (dst), (src), (size_t)(bytes))) return -1; \
+  } while (0)
+#define MR_D2H(dst, src, bytes, s)                                         \
+  do {                                                                     \
+    if (::mr::t_stager.d2h((s), (dst), (src), (size_t)(bytes))) return -1; \
+  } while (0)
+
 constexpr int kMaxK = 128;        // largest factor count the Gram kernel tiles
 // Row stride of factor tables / CG vectors: k rounded up to a multiple of 16
 // (one 16-wide block of the tri16 storage), so every Gram lane's NB-float segment of a row

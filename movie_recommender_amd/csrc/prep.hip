@@ -359,18 +359,18 @@ static int prep_init(Prep* P, int device, int64_t n, const int* uid, const int* 
   MR_HIP(hipMalloc((void**)&P->r, nn * 8));
   MR_HIP(hipMalloc((void**)&P->alive, nn));
   if (n) {
-    MR_HIP(hipMemcpyAsync(P->uid, uid, n * 4, hipMemcpyHostToDevice, P->s));
-    MR_HIP(hipMemcpyAsync(P->mid, mid, n * 4, hipMemcpyHostToDevice, P->s));
-    MR_HIP(hipMemcpyAsync(P->r, r, n * 8, hipMemcpyHostToDevice, P->s));
+    MR_H2D(P->uid, uid, n * 4, P->s);
+    MR_H2D(P->mid, mid, n * 4, P->s);
+    MR_H2D(P->r, r, n * 8, P->s);
   }
   PBuf<int> mx;
   if (mx.alloc(3)) return -1;
   const int init[3] = {-1, -1, 0};
-  MR_HIP(hipMemcpyAsync(mx.p, init, sizeof init, hipMemcpyHostToDevice, P->s));
+  MR_H2D(mx.p, init, sizeof init, P->s);
   prep_bounds_kernel<<<pgrid(n), 256, 0, P->s>>>(n, P->uid, P->mid, mx.p);
   MR_HIP(hipGetLastError());
   int h[3];
-  MR_HIP(hipMemcpyAsync(h, mx.p, sizeof h, hipMemcpyDeviceToHost, P->s));
+  MR_D2H(h, mx.p, sizeof h, P->s);
   MR_HIP(hipStreamSynchronize(P->s));
   MR_CHECK(h[2] == 0, "prep: user and movie ids must be >= 0");
   P->U = h[0] + 1;
@@ -410,10 +410,10 @@ static int prep_medians(Prep* P, double* med_out) {
     MR_HIP(hipGetLastError());
   } else {
     std::vector<double> nanv(M, NAN);
-    MR_HIP(hipMemcpyAsync(med.p, nanv.data(), M * 8, hipMemcpyHostToDevice, P->s));
+    MR_H2D(med.p, nanv.data(), M * 8, P->s);
   }
   if (P->mark()) return -1;
-  MR_HIP(hipMemcpyAsync(med_out, med.p, (size_t)M * 8, hipMemcpyDeviceToHost, P->s));
+  MR_D2H(med_out, med.p, (size_t)M * 8, P->s);
   return P->end();
 }
 
@@ -489,16 +489,16 @@ static int prep_shrink(Prep* P, int k, int restart, unsigned char* keep, int* ro
       prep_kill_dec_kernel<<<pgrid(n), 256, 0, P->s>>>(n, P->uid, P->mid, present.p, dead.p,
                                                        P->alive, P->ucnt, P->mcnt);
     MR_HIP(hipGetLastError());
-    MR_HIP(hipMemcpyAsync(h, flag.p, 8, hipMemcpyDeviceToHost, P->s));
+    MR_D2H(h, flag.p, 8, P->s);
     MR_HIP(hipStreamSynchronize(P->s));
   } while (h[0] || h[1]);
   // survivors: every present user now has >= k+1 ratings and every counted
   // movie >= k (the last round changed nothing)
   if (P->mark()) return -1;
   std::vector<int> uc(U), mc(M);
-  MR_HIP(hipMemcpyAsync(uc.data(), P->ucnt, (size_t)U * 4, hipMemcpyDeviceToHost, P->s));
-  MR_HIP(hipMemcpyAsync(mc.data(), P->mcnt, (size_t)M * 4, hipMemcpyDeviceToHost, P->s));
-  if (keep && n) MR_HIP(hipMemcpyAsync(keep, P->alive, n, hipMemcpyDeviceToHost, P->s));
+  MR_D2H(uc.data(), P->ucnt, (size_t)U * 4, P->s);
+  MR_D2H(mc.data(), P->mcnt, (size_t)M * 4, P->s);
+  if (keep && n) MR_D2H(keep, P->alive, n, P->s);
   if (P->end()) return -1;
   long long nk = 0;
   int nu = 0, nm = 0;
@@ -526,7 +526,7 @@ static int prep_first(Prep* P, int n_chunks, const long long* cb, long long* fu_
   PBuf<int64_t> dcb;
   const int64_t nu = (int64_t)n_chunks * P->U, nm = (int64_t)n_chunks * P->M;
   if (fu.alloc(nu) || fm.alloc(nm) || dcb.alloc(n_chunks + 1)) return -1;
-  MR_HIP(hipMemcpyAsync(dcb.p, cb, (n_chunks + 1) * 8, hipMemcpyHostToDevice, P->s));
+  MR_H2D(dcb.p, cb, (n_chunks + 1) * 8, P->s);
   const unsigned long long inf = 0x7fffffffffffffffull;
   prep_fill_u64_kernel<<<pgrid(nu), 256, 0, P->s>>>(nu, fu.p, inf);
   prep_fill_u64_kernel<<<pgrid(nm), 256, 0, P->s>>>(nm, fm.p, inf);
@@ -538,8 +538,8 @@ static int prep_first(Prep* P, int n_chunks, const long long* cb, long long* fu_
   }
   MR_HIP(hipGetLastError());
   if (P->mark()) return -1;
-  MR_HIP(hipMemcpyAsync(fu_out, fu.p, nu * 8, hipMemcpyDeviceToHost, P->s));
-  MR_HIP(hipMemcpyAsync(fm_out, fm.p, nm * 8, hipMemcpyDeviceToHost, P->s));
+  MR_D2H(fu_out, fu.p, nu * 8, P->s);
+  MR_D2H(fm_out, fm.p, nm * 8, P->s);
   return P->end();
 }
 
@@ -554,9 +554,9 @@ static int prep_convert(Prep* P, const int* umap, const int* mmap, const double*
   if (flags.alloc(n) || pos.alloc(n) || du.alloc(P->U) || dm.alloc(P->M) || bad.alloc(1) ||
       dou.alloc(nk) || dom.alloc(nk) || dmed.alloc(P->M) || dor.alloc(nk))
     return -1;
-  MR_HIP(hipMemcpyAsync(du.p, umap, (size_t)P->U * 4, hipMemcpyHostToDevice, P->s));
-  MR_HIP(hipMemcpyAsync(dm.p, mmap, (size_t)P->M * 4, hipMemcpyHostToDevice, P->s));
-  MR_HIP(hipMemcpyAsync(dmed.p, med_h, (size_t)P->M * 8, hipMemcpyHostToDevice, P->s));
+  MR_H2D(du.p, umap, (size_t)P->U * 4, P->s);
+  MR_H2D(dm.p, mmap, (size_t)P->M * 4, P->s);
+  MR_H2D(dmed.p, med_h, (size_t)P->M * 8, P->s);
   MR_HIP(hipMemsetAsync(bad.p, 0, 4, P->s));
   if (n) {
     prep_u8_to_i64_kernel<<<pgrid(n), 256, 0, P->s>>>(n, P->alive, flags.p);
@@ -574,11 +574,11 @@ static int prep_convert(Prep* P, const int* umap, const int* mmap, const double*
   }
   if (P->mark()) return -1;
   int hb = 0;
-  MR_HIP(hipMemcpyAsync(&hb, bad.p, 4, hipMemcpyDeviceToHost, P->s));
+  MR_D2H(&hb, bad.p, 4, P->s);
   if (nk) {
-    MR_HIP(hipMemcpyAsync(ou, dou.p, nk * 4, hipMemcpyDeviceToHost, P->s));
-    MR_HIP(hipMemcpyAsync(om, dom.p, nk * 4, hipMemcpyDeviceToHost, P->s));
-    MR_HIP(hipMemcpyAsync(orr, dor.p, nk * 8, hipMemcpyDeviceToHost, P->s));
+    MR_D2H(ou, dou.p, nk * 4, P->s);
+    MR_D2H(om, dom.p, nk * 4, P->s);
+    MR_D2H(orr, dor.p, nk * 8, P->s);
   }
   if (P->end()) return -1;
   MR_CHECK(hb == 0, "prep: a surviving user or movie has no entry in the id map");

@@ -705,7 +705,7 @@ struct DBuf {   // call-scoped device buffer
   }
   int upload(const T* h, int64_t n, hipStream_t s) {
     if (alloc(n)) return -1;
-    if (n > 0) MR_HIP(hipMemcpyAsync(p, h, n * sizeof(T), hipMemcpyHostToDevice, s));
+    if (n > 0) MR_H2D(p, h, n * sizeof(T), s);
     return 0;
   }
 };
@@ -754,11 +754,11 @@ static int rec_init(Rec* r, int device, int k, int n_als, const double* Vh, int 
   MR_HIP(hipMalloc((void**)&r->Vc, nc * k * sizeof(double)));
   MR_HIP(hipMalloc((void**)&r->med, nc * sizeof(double)));
   MR_HIP(hipMalloc((void**)&r->mid, nc * sizeof(int)));
-  if (n_als) MR_HIP(hipMemcpyAsync(r->V, Vh, (size_t)n_als * k * 8, hipMemcpyHostToDevice, r->stream));
+  if (n_als) MR_H2D(r->V, Vh, (size_t)n_als * k * 8, r->stream);
   if (n_cand) {
-    MR_HIP(hipMemcpyAsync(r->Vc, vc.data(), vc.size() * 8, hipMemcpyHostToDevice, r->stream));
-    MR_HIP(hipMemcpyAsync(r->med, cand_med, (size_t)n_cand * 8, hipMemcpyHostToDevice, r->stream));
-    MR_HIP(hipMemcpyAsync(r->mid, cand_mid, (size_t)n_cand * 4, hipMemcpyHostToDevice, r->stream));
+    MR_H2D(r->Vc, vc.data(), vc.size() * 8, r->stream);
+    MR_H2D(r->med, cand_med, (size_t)n_cand * 8, r->stream);
+    MR_H2D(r->mid, cand_mid, (size_t)n_cand * 4, r->stream);
   }
   MR_HIP(hipStreamSynchronize(r->stream));
   return 0;
@@ -784,7 +784,7 @@ static int rec_scores(Rec* r, int n_users, const double* Xh, double* out) {
   if (X.alloc(B * K) || S.alloc(B * r->n_cand)) return -1;
   for (int64_t u0 = 0; u0 < n_users; u0 += B) {
     const int nb = (int)std::min<int64_t>(B, n_users - u0);
-    MR_HIP(hipMemcpyAsync(X.p, Xh + u0 * K, (size_t)nb * K * 8, hipMemcpyHostToDevice, r->stream));
+    MR_H2D(X.p, Xh + u0 * K, (size_t)nb * K * 8, r->stream);
     const dim3 grid((r->n_cand + SC_C - 1) / SC_C, (nb + SC_U - 1) / SC_U);
     if (timed(r, RT_SCORE, [&]() {
           rec_score_kernel<false><<<grid, 256, 0, r->stream>>>(nb, r->n_cand, r->k, X.p, r->Vc,
@@ -793,8 +793,7 @@ static int rec_scores(Rec* r, int n_users, const double* Xh, double* out) {
           return 0;
         }))
       return -1;
-    MR_HIP(hipMemcpyAsync(out + u0 * r->n_cand, S.p, (size_t)nb * r->n_cand * 8,
-                          hipMemcpyDeviceToHost, r->stream));
+    MR_D2H(out + u0 * r->n_cand, S.p, (size_t)nb * r->n_cand * 8, r->stream);
   }
   MR_HIP(hipStreamSynchronize(r->stream));
   return 0;
@@ -834,7 +833,7 @@ static int rec_top_n(Rec* r, int n_users, const double* Xh, const long long* exc
   std::vector<int64_t> loc;
   for (int64_t u0 = 0; u0 < n_users; u0 += B) {
     const int nb = (int)std::min<int64_t>(B, n_users - u0);
-    MR_HIP(hipMemcpyAsync(X.p, Xh + u0 * K, (size_t)nb * K * 8, hipMemcpyHostToDevice, r->stream));
+    MR_H2D(X.p, Xh + u0 * K, (size_t)nb * K * 8, r->stream);
     const dim3 grid((r->n_cand + SC_C - 1) / SC_C, (nb + SC_U - 1) / SC_U);
     if (timed(r, RT_SCORE, [&]() {
           rec_range_init_kernel<<<(nb + 255) / 256, 256, 0, r->stream>>>(nb, kmin.p, kmax.p);
@@ -847,10 +846,9 @@ static int rec_top_n(Rec* r, int n_users, const double* Xh, const long long* exc
     if (excl_off) {
       loc.assign(nb + 1, 0);
       for (int i = 0; i <= nb; ++i) loc[i] = excl_off[u0 + i] - excl_off[u0];
-      MR_HIP(hipMemcpyAsync(eoff.p, loc.data(), (nb + 1) * 8, hipMemcpyHostToDevice, r->stream));
+      MR_H2D(eoff.p, loc.data(), (nb + 1) * 8, r->stream);
       if (loc[nb] > 0)
-        MR_HIP(hipMemcpyAsync(ecand.p, excl_cand + excl_off[u0], loc[nb] * 4,
-                              hipMemcpyHostToDevice, r->stream));
+        MR_H2D(ecand.p, excl_cand + excl_off[u0], loc[nb] * 4, r->stream);
       if (timed(r, RT_EXCL, [&]() {
             rec_exclude_kernel<<<nb, 256, 0, r->stream>>>(S.p, r->n_cand, eoff.p, ecand.p);
             return 0;
@@ -864,9 +862,9 @@ static int rec_top_n(Rec* r, int n_users, const double* Xh, const long long* exc
           return 0;
         }))
       return -1;
-    MR_HIP(hipMemcpyAsync(out_mid + u0 * N, omid.p, (size_t)nb * N * 4, hipMemcpyDeviceToHost, r->stream));
-    MR_HIP(hipMemcpyAsync(out_score + u0 * N, osc.p, (size_t)nb * N * 8, hipMemcpyDeviceToHost, r->stream));
-    MR_HIP(hipMemcpyAsync(out_count + u0, ocnt.p, (size_t)nb * 4, hipMemcpyDeviceToHost, r->stream));
+    MR_D2H(out_mid + u0 * N, omid.p, (size_t)nb * N * 4, r->stream);
+    MR_D2H(out_score + u0 * N, osc.p, (size_t)nb * N * 8, r->stream);
+    MR_D2H(out_count + u0, ocnt.p, (size_t)nb * 4, r->stream);
   }
   MR_HIP(hipStreamSynchronize(r->stream));
   for (int u = 0; u < n_users; ++u)
@@ -909,7 +907,7 @@ static int rec_fold_in(Rec* r, int n_users, const long long* off, const int* als
       }))
     return -1;
   std::vector<int> meth(n_users);
-  MR_HIP(hipMemcpyAsync(meth.data(), dmeth.p, n_users * 4, hipMemcpyDeviceToHost, r->stream));
+  MR_D2H(meth.data(), dmeth.p, n_users * 4, r->stream);
   MR_HIP(hipStreamSynchronize(r->stream));
   std::vector<int> flagged;
   std::vector<int64_t> soff(1, 0);
@@ -936,7 +934,7 @@ static int rec_fold_in(Rec* r, int n_users, const long long* off, const int* als
         }))
       return -1;
   }
-  MR_HIP(hipMemcpyAsync(Xout, dX.p, (size_t)n_users * K * 8, hipMemcpyDeviceToHost, r->stream));
+  MR_D2H(Xout, dX.p, (size_t)n_users * K * 8, r->stream);
   MR_HIP(hipStreamSynchronize(r->stream));
   if (method_out) std::copy(meth.begin(), meth.end(), method_out);
   return 0;
@@ -972,12 +970,12 @@ static int rec_evaluate(Rec* r, int n_rows, const double* Uh, int n_test, const 
         return 0;
       }))
     return -1;
-  MR_HIP(hipMemcpyAsync(agreement, dagr.p, n_test * 8, hipMemcpyDeviceToHost, r->stream));
-  MR_HIP(hipMemcpyAsync(n_agree, dag.p, n_test * 8, hipMemcpyDeviceToHost, r->stream));
-  MR_HIP(hipMemcpyAsync(n_dis, ddis.p, n_test * 8, hipMemcpyDeviceToHost, r->stream));
-  if (pred) MR_HIP(hipMemcpyAsync(pred, dpred.p, nnz * 8, hipMemcpyDeviceToHost, r->stream));
-  if (sse) MR_HIP(hipMemcpyAsync(sse, dsse.p, n_test * 8, hipMemcpyDeviceToHost, r->stream));
-  if (n_pred) MR_HIP(hipMemcpyAsync(n_pred, dnp.p, n_test * 8, hipMemcpyDeviceToHost, r->stream));
+  MR_D2H(agreement, dagr.p, n_test * 8, r->stream);
+  MR_D2H(n_agree, dag.p, n_test * 8, r->stream);
+  MR_D2H(n_dis, ddis.p, n_test * 8, r->stream);
+  if (pred) MR_D2H(pred, dpred.p, nnz * 8, r->stream);
+  if (sse) MR_D2H(sse, dsse.p, n_test * 8, r->stream);
+  if (n_pred) MR_D2H(n_pred, dnp.p, n_test * 8, r->stream);
   MR_HIP(hipStreamSynchronize(r->stream));
   return 0;
 }
@@ -1006,9 +1004,9 @@ static int rank_agreement(int device, int n_users, const long long* off, const d
                                                  nullptr, nullptr, dpred.p, dagr.p, dag.p,
                                                  ddis.p, nullptr, nullptr);
   MR_HIP(hipGetLastError());
-  MR_HIP(hipMemcpyAsync(agreement, dagr.p, n_users * 8, hipMemcpyDeviceToHost, s));
-  if (n_agree) MR_HIP(hipMemcpyAsync(n_agree, dag.p, n_users * 8, hipMemcpyDeviceToHost, s));
-  if (n_dis) MR_HIP(hipMemcpyAsync(n_dis, ddis.p, n_users * 8, hipMemcpyDeviceToHost, s));
+  MR_D2H(agreement, dagr.p, n_users * 8, s);
+  if (n_agree) MR_D2H(n_agree, dag.p, n_users * 8, s);
+  if (n_dis) MR_D2H(n_dis, ddis.p, n_users * 8, s);
   MR_HIP(hipStreamSynchronize(s));
   return 0;
 }

@@ -355,14 +355,14 @@ static int sim_init(Similar* S, int device, int M, int U, const long long* off, 
   MR_HIP(hipMalloc((void**)&S->ustart, (size_t)std::max(U, 1) * (S->NR + 1) * 4));
   MR_HIP(hipMalloc((void**)&S->gmask, mm * 8));
   MR_HIP(hipMalloc((void**)&S->ghas, mm));
-  MR_HIP(hipMemcpyAsync(S->moff, off, ((size_t)M + 1) * 8, hipMemcpyHostToDevice, S->s));
+  MR_H2D(S->moff, off, ((size_t)M + 1) * 8, S->s);
   if (nnz) {
-    MR_HIP(hipMemcpyAsync(S->muser, user, nnz * 4, hipMemcpyHostToDevice, S->s));
-    MR_HIP(hipMemcpyAsync(S->mr2, r2, nnz, hipMemcpyHostToDevice, S->s));
+    MR_H2D(S->muser, user, nnz * 4, S->s);
+    MR_H2D(S->mr2, r2, nnz, S->s);
   }
   if (M) {
-    MR_HIP(hipMemcpyAsync(S->gmask, gmask, (size_t)M * 8, hipMemcpyHostToDevice, S->s));
-    MR_HIP(hipMemcpyAsync(S->ghas, ghas, M, hipMemcpyHostToDevice, S->s));
+    MR_H2D(S->gmask, gmask, (size_t)M * 8, S->s);
+    MR_H2D(S->ghas, ghas, M, S->s);
   }
   // user lists sorted by movie index (one 64-bit radix sort)
   SBuf<uint64_t> k0, k1;
@@ -400,8 +400,8 @@ static int sim_find(Similar* S, int n_query, const int* query, const double* boo
   if ((query && dq.alloc(n_query)) || db.alloc(n_boost) || dj.alloc((int64_t)n_query * nres) ||
       ds.alloc((int64_t)n_query * nres) || dc.alloc(n_query))
     return -1;
-  if (query) MR_HIP(hipMemcpyAsync(dq.p, query, n_query * 4, hipMemcpyHostToDevice, S->s));
-  MR_HIP(hipMemcpyAsync(db.p, boost1, (size_t)n_boost * 8, hipMemcpyHostToDevice, S->s));
+  if (query) MR_H2D(dq.p, query, n_query * 4, S->s);
+  MR_H2D(db.p, boost1, (size_t)n_boost * 8, S->s);
   const size_t lds = 2 * SM_RS * 8 + SM_CAP * (4 + 4 + 8);
   MR_HIP(hipFuncSetAttribute((const void*)sim_find_kernel,
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -412,9 +412,9 @@ static int sim_find(Similar* S, int n_query, const int* query, const double* boo
                                                  nres, dj.p, ds.p, dc.p);
   MR_HIP(hipGetLastError());
   MR_HIP(hipEventRecord(S->ev[1], S->s));
-  MR_HIP(hipMemcpyAsync(out_j, dj.p, (size_t)n_query * nres * 4, hipMemcpyDeviceToHost, S->s));
-  MR_HIP(hipMemcpyAsync(out_s, ds.p, (size_t)n_query * nres * 8, hipMemcpyDeviceToHost, S->s));
-  MR_HIP(hipMemcpyAsync(out_cnt, dc.p, (size_t)n_query * 4, hipMemcpyDeviceToHost, S->s));
+  MR_D2H(out_j, dj.p, (size_t)n_query * nres * 4, S->s);
+  MR_D2H(out_s, ds.p, (size_t)n_query * nres * 8, S->s);
+  MR_D2H(out_cnt, dc.p, (size_t)n_query * 4, S->s);
   MR_HIP(hipStreamSynchronize(S->s));
   float t = 0.f;
   MR_HIP(hipEventElapsedTime(&t, S->ev[0], S->ev[1]));

@@ -171,6 +171,28 @@ class AlsContext:
             G.ctypes.data_as(_lib.DP), c.ctypes.data_as(_lib.DP)), "mr_als_get_normal_equations")
         return G, c
 
+    def layout(self, side):
+        """The side's device CSR (off, idx, val) and Gram work list
+        (begin, len, entity, slab) as built on the GPU."""
+        L = _lib.lib()
+        user = side in (0, "users")
+        sd = 0 if user else 1
+        E = self.num_users if user else self.num_items
+        off = np.empty(E + 1, np.int64)
+        _lib.check(L.mr_als_get_layout(self._h, sd, off.ctypes.data_as(_lib.LLP), None, None,
+                                       None, None, None, None), "mr_als_get_layout")
+        nnz = int(off[-1])
+        nw = int(L.mr_als_work_items(self._h, sd))
+        idx = np.empty(nnz, np.int32)
+        val = np.empty(nnz, np.float32)
+        wb = np.empty(nw, np.int64)
+        wl, we, ws = (np.empty(nw, np.int32) for _ in range(3))
+        _lib.check(L.mr_als_get_layout(
+            self._h, sd, None, idx.ctypes.data_as(_lib.IP), val.ctypes.data_as(_lib.FP),
+            wb.ctypes.data_as(_lib.LLP), wl.ctypes.data_as(_lib.IP), we.ctypes.data_as(_lib.IP),
+            ws.ctypes.data_as(_lib.IP)), "mr_als_get_layout")
+        return off, idx, val, (wb, wl, we, ws)
+
     def cg_vectors(self, side):
         """(r, p, q) of the side's last CG solve, fp64 (users: k+1 per user)."""
         user = side in (0, "users")

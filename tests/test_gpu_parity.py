@@ -458,3 +458,50 @@ def test_full_size_gram_sampled(gpu):
                 assert np.max(np.abs(c[t] - cr)) / max(np.max(np.abs(cr)), 1.0) < 2e-5
         its, rr = ctx.half_step("users")
         assert its >= 1 and np.isfinite(rr)
+
+
+def expected_layout(ids, other, ratings, E, chunk=2048):
+    """Host restatement of the context build: stable CSR by entity, then the
+    Gram work list (entities longer than `chunk` split into slabs numbered in
+    entity order; stable sort by length, heavy first) -- engine.hip build_side."""
+    order = np.argsort(ids, kind="stable")
+    off = np.zeros(E + 1, np.int64)
+    np.cumsum(np.bincount(ids, minlength=E), out=off[1:])
+    work = []
+    nslab = 0
+    for e in range(E):
+        ln = int(off[e + 1] - off[e])
+        if ln <= chunk:
+            work.append((int(off[e]), ln, e, -1))
+        else:
+            nc = (ln + chunk - 1) // chunk
+            for c in range(nc):
+                b = int(off[e]) + c * chunk
+                work.append((b, min(chunk, int(off[e + 1]) - b), e, nslab + c))
+            nslab += nc
+    work.sort(key=lambda w: -w[1])     # stable: equal lengths keep entity order
+    return off, other[order].astype(np.int32), ratings[order].astype(np.float32), work
+
+
+def test_full_size_context_build_exact(gpu):
+    """BASELINE.json configs[2] size: the device CSR of both sides and the
+    Gram work lists read back and compared with their host restatement, bit
+    for bit (uploads go through pinned staging, Stager in xfer.hip)."""
+    from movie_recommender_amd import synth
+    from movie_recommender_amd.engine import AlsContext
+    k = 64
+    rs = synth.movielens_like("ml-full", k)
+    with AlsContext(rs.user_ids, rs.item_ids, rs.ratings, k, rs.num_users,
+                    rs.num_items) as ctx:
+        for side in ("users", "items"):
+            ids, other, E = ((rs.user_ids, rs.item_ids, rs.num_users) if side == "users"
+                             else (rs.item_ids, rs.user_ids, rs.num_items))
+            off, idx, val, (wb, wl, we, ws) = ctx.layout(side)
+            eoff, eidx, eval_, work = expected_layout(ids, other, rs.ratings, E)
+            assert np.array_equal(off, eoff), side
+            assert np.array_equal(idx, eidx), side
+            assert np.array_equal(val, eval_), side
+            w = np.array(work, np.int64)
+            assert len(wb) == len(w), side
+            assert np.array_equal(wb, w[:, 0]) and np.array_equal(wl, w[:, 1]), side
+            assert np.array_equal(we, w[:, 2]) and np.array_equal(ws, w[:, 3]), side
