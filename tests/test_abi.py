@@ -3,6 +3,7 @@ import ctypes
 import os
 import re
 
+import numpy as np
 import pytest
 
 from conftest import ROOT
@@ -64,3 +65,44 @@ def test_no_gpu_means_clean_error():
     u = np.zeros(4, np.int32)
     with pytest.raises(RuntimeError):
         cpp_ls.als(u, u, np.ones(4), 1, 1, 1)
+
+
+@pytest.mark.gpu
+def test_reference_wrapper_calling_convention(gpu):
+    """The library called exactly as the reference wrapper does
+    (cpp/python/cpp_ls.py:89-167): a fresh CDLL with NO argtypes / restype,
+    bare Python ints, ``ctypes.c_double(...)`` for min_r_decrease, id arrays
+    passed as POINTER(c_double), ``ctypes.byref`` for final_rr."""
+    import ctypes
+    from movie_recommender_amd import _lib
+    from conftest import load_golden, rel_err
+    dll = ctypes.CDLL(_lib.LIB_PATH)      # no prototypes declared on this handle
+    dll.set_thread_count(77)
+    assert dll.get_thread_count() == 77
+    d = load_golden("als_dense_40x45_k3.npz")
+    uid = np.ascontiguousarray(d["user_ids"], np.int32)
+    iid = np.ascontiguousarray(d["item_ids"], np.int32)
+    r = np.ascontiguousarray(d["ratings"], np.float64)
+    U = np.array(d["U0"], np.float64)
+    V = np.array(d["V0"], np.float64)
+    dp = ctypes.POINTER(ctypes.c_double)
+    it = dll.als_from_python(uid.ctypes.data_as(dp), iid.ctypes.data_as(dp), len(r),
+                             r.ctypes.data_as(dp), 3, len(U), U.ctypes.data_as(dp), len(V),
+                             V.ctypes.data_as(dp), ctypes.c_double(0.01), 200, 1)
+    assert it == int(d["ret"])
+    assert rel_err(U, d["U"]) <= 1e-5 and rel_err(V, d["V"]) <= 1e-5
+    g = load_golden("cg_dense_200x50.npz")
+    rp = np.ascontiguousarray(g["row_ptr"], np.int32)
+    ci = np.ascontiguousarray(g["col_idx"], np.int32)
+    v = np.ascontiguousarray(g["vals"], np.float64)
+    b = np.ascontiguousarray(g["b"], np.float64)
+    x = np.array(g["x0"], np.float64).reshape(-1, 1)
+    ip = ctypes.POINTER(ctypes.c_int)
+    final_rr = ctypes.c_double(0)
+    it = dll.cg_least_squares_from_python(len(rp) - 1, int(g["ncols"]), rp.ctypes.data_as(ip),
+                                          ci.ctypes.data_as(ip), v.ctypes.data_as(dp), len(b),
+                                          b.ctypes.data_as(dp), int(g["ncols"]),
+                                          x.ctypes.data_as(dp), ctypes.c_double(0.01), 200,
+                                          ctypes.byref(final_rr))
+    assert it == int(g["iterations"])
+    assert rel_err(x.ravel(), g["x"]) <= 1e-9

@@ -87,3 +87,60 @@ def test_edge_cases(gpu):
     # medians of even counts are the mean of the two middle ratings
     assert prep.movie_medians([(1, [(4, 1.0), (5, 2.0)]), (2, [(4, 4.0), (5, 2.5)])]) == \
         {4: 2.5, 5: 2.25}
+
+
+def test_prep_then_train_writes_reference_factor_files(gpu, tmp_path):
+    """``als_data_set_shrink`` -> ``als_train`` (movie_lens_data.py:547-713):
+    the training files written by prep feed training, whose pickled factor
+    vectors are the device run on exactly those arrays from the same
+    global-RNG draws (U0 before V0, factor by factor).  The prep fixture is
+    realistic, ill-conditioned data: the reference's own factors move by tens
+    of percent between thread counts there, so quality is checked as the
+    training RMSE against the band of the compiled reference
+    (oracle/_ref) at 1, 2 and 8 threads from the same initial factors."""
+    from movie_recommender_amd import prep, train
+    from movie_recommender_amd.engine import AlsContext
+    from oracle import als_oracle, ref
+    d = fixture(1)
+    factors = d["factors"].tolist()
+    res = prep.als_data_set_shrink(d["train"], d["test"], d["medians"], factors,
+                                   out_dir=str(tmp_path))
+    state = np.random.get_state()
+    try:
+        np.random.seed(5)
+        out = train.als_train(factors, str(tmp_path), verbose=False)
+        np.random.seed(5)
+        inits = {}
+        for k in factors:
+            r = res[k]
+            nU, nI = len(r.als_user_ids), len(r.als_movie_ids)
+            inits[k] = (np.random.uniform(-1, 1, nU * (k + 1)), np.random.uniform(-1, 1, nI * k))
+    finally:
+        np.random.set_state(state)
+    for k in factors:
+        r = res[k]
+        nU, nI = len(r.als_user_ids), len(r.als_movie_ids)
+        U0, V0 = inits[k]
+        with open(tmp_path / f"als{k}_user_factors.bin", "rb") as f:
+            U = pickle.load(f)
+        with open(tmp_path / f"als{k}_item_factors.bin", "rb") as f:
+            V = pickle.load(f)
+        assert U.dtype == np.float64 and U.shape == (nU * (k + 1),)
+        assert V.dtype == np.float64 and V.shape == (nI * k,)
+        assert np.array_equal(U, out[k][0]) and np.array_equal(V, out[k][1])
+        with AlsContext(r.user_ids_train, r.movie_ids_train, r.ratings_train, k, nU, nI) as ctx:
+            ctx.set_factors(U0, V0)
+            ret = ctx.run()
+            Ud, Vd = ctx.get_factors()
+        assert ret == out[k][2]
+        assert np.array_equal(U, Ud) and np.array_equal(V, Vd)
+        args = (r.user_ids_train, r.movie_ids_train, r.ratings_train, k)
+        band = []
+        for tc in (1, 2, 8):
+            ref.set_thread_count(tc)
+            Ur, Vr, _ = ref.als(*args, U0, V0)
+            band.append(als_oracle.rmse(Ur, Vr, *args[:3], k))
+        ref.set_thread_count(1)
+        got = als_oracle.rmse(U, V, *args[:3], k)
+        lo, hi = min(band), max(band)
+        assert 0.8 * lo <= got <= 1.25 * hi, (k, got, band)

@@ -1,6 +1,6 @@
 """Microbenchmark of the Gram (normal-equation) kernels and one CG half-step
 on the bench workload.  python tools/gram_bench.py [--k 64] [--reps 5]
-(MR_GRAM_G selects the pipeline group size; see kernels.hip)."""
+(the Gram runs the bf16x3 matrix-core loop)."""
 import argparse, json, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
