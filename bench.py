@@ -2,7 +2,13 @@
 (BASELINE.json metric), MovieLens-full shape, k = 64, on MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--k 64]
-                    [--shape ml-full] [--solver cg|cholesky] [--no-cpu]
+                    [--shape ml-full|c5] [--scale S] [--solver cg|cholesky] [--no-cpu]
+
+``--shape c5`` is BASELINE.json configs[4] (synthetic 10 M users x 1 M items x
+1e9 ratings; use --k 128): streamed by ``synth.C5Generator`` -- every rank
+regenerates only its own user view and its items' view, factors are seeded on
+the device -- and ``--scale`` runs a fraction of it (1/8 = one rank's users and
+ratings of the 8-GPU run, on one GPU).
 
 A step is one full ALS iteration of the reference loop (user half-step:
 normal equations from gathered item rows + global block-CG solve; item
@@ -147,7 +153,8 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--k", type=int, default=64)
-    ap.add_argument("--shape", default="ml-full")
+    ap.add_argument("--shape", default="ml-full", choices=["ml-full", "ml-100k", "c5"])
+    ap.add_argument("--scale", type=float, default=1.0, help="fraction of the c5 shape")
     ap.add_argument("--solver", default="cg", choices=["cg", "cholesky"])
     ap.add_argument("--ridge", type=float, default=0.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -176,28 +183,53 @@ def main():
     from movie_recommender_amd.distributed import sharded_context
 
     t0 = time.perf_counter()
-    if dist is not None and rank != 0:
-        dist.barrier()            # rank 0 generates (or loads) the data first
-    rs = load_data(args.shape, args.k)
-    if dist is not None and rank == 0:
-        dist.barrier()
     k = args.k
-    log(f"[bench] data {args.shape} k={k}: N={rs.n} users={rs.num_users} "
-        f"items={rs.num_items} ({time.perf_counter() - t0:.1f} s)")
-    rng = np.random.RandomState(0)
-    U0 = rng.uniform(-1, 1, rs.num_users * (k + 1))
-    V0 = rng.uniform(-1, 1, rs.num_items * k)
+    c5 = args.shape == "c5"
+    if c5:
+        gen = synth.C5Generator(scale=args.scale)
+        n_total, n_users, n_items = gen.n, gen.num_users, gen.num_items
+    else:
+        if dist is not None and rank != 0:
+            dist.barrier()            # rank 0 generates (or loads) the data first
+        rs = load_data(args.shape, k)
+        if dist is not None and rank == 0:
+            dist.barrier()
+        n_total, n_users, n_items = rs.n, rs.num_users, rs.num_items
+    log(f"[bench] data {args.shape} k={k}: N={n_total} users={n_users} "
+        f"items={n_items} ({time.perf_counter() - t0:.1f} s)")
 
     t0 = time.perf_counter()
-    if dist is not None:
-        ctx = sharded_context(rs.user_ids, rs.item_ids, rs.ratings, k, rs.num_users,
-                              rs.num_items, local_rank, "rccl", solver=args.solver,
-                              ridge=args.ridge)
+    if c5:
+        from movie_recommender_amd.distributed import attach_rccl, entity_cost, shard_bounds
+        if dist is not None:
+            ub = shard_bounds(entity_cost(gen.deg, k), world)
+            ib = shard_bounds(entity_cost(np.rint(gen.expected_item_counts()).astype(np.int64),
+                                          k), world)
+            u0, u1, i0, i1 = int(ub[rank]), int(ub[rank + 1]), int(ib[rank]), int(ib[rank + 1])
+            uv = gen.user_view(u0, u1)
+            iv = gen.item_view(i0, i1)
+            ctx = AlsContext(uv[0], uv[1], uv[2], k, n_users, n_items, device=local_rank,
+                             solver=args.solver, ridge=args.ridge, user_range=(u0, u1),
+                             item_range=(i0, i1), item_view=iv)
+            del uv, iv
+            attach_rccl(ctx, rank, world, ub, ib)
+        else:
+            u, i, r = gen.all_ratings()
+            ctx = AlsContext(u, i, r, k, n_users, n_items, device=local_rank,
+                             solver=args.solver, ridge=args.ridge)
+            del u, i, r
+        ctx.init_factors(0)
     else:
-        ctx = AlsContext(rs.user_ids, rs.item_ids, rs.ratings, k, rs.num_users,
-                         rs.num_items, device=local_rank, solver=args.solver,
-                         ridge=args.ridge)
-    ctx.set_factors(U0, V0)
+        rng = np.random.RandomState(0)
+        U0 = rng.uniform(-1, 1, n_users * (k + 1))
+        V0 = rng.uniform(-1, 1, n_items * k)
+        if dist is not None:
+            ctx = sharded_context(rs.user_ids, rs.item_ids, rs.ratings, k, n_users, n_items,
+                                  local_rank, "rccl", solver=args.solver, ridge=args.ridge)
+        else:
+            ctx = AlsContext(rs.user_ids, rs.item_ids, rs.ratings, k, n_users, n_items,
+                             device=local_rank, solver=args.solver, ridge=args.ridge)
+        ctx.set_factors(U0, V0)
     ctx.sync()
     log(f"[bench] context built in {time.perf_counter() - t0:.2f} s")
 
@@ -214,7 +246,8 @@ def main():
 
     # snapshot of the iterate: the event-free pass below replays the SAME
     # steps (bit-identical kernels, so identical CG iteration counts)
-    snap = ctx.get_factors() if not args.no_kernel_events else None
+    replay = not args.no_kernel_events and n_users * (k + 1) + n_items * k < 200_000_000
+    snap = ctx.get_factors() if replay else None
     barrier()
     t_start = time.perf_counter()
     for s in range(args.steps):
@@ -233,7 +266,7 @@ def main():
     # cost a few us per launch).
     plain_ms = None
     replay_identical = None
-    if not args.no_kernel_events:
+    if replay:
         ctx.set_factors(*snap)
         ctx.reset_stats()
         barrier()
@@ -253,7 +286,7 @@ def main():
 
     # local work units (ratings processed by this rank per iteration)
     n_local_users = ctx.num_ratings
-    total_ratings = rs.n
+    total_ratings = n_total
     value = total_ratings * args.steps / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
 
@@ -266,8 +299,8 @@ def main():
     cls, tot_ms = best
     launches = max(1, st["kernel_launches"][cls])
     avg_s = tot_ms / launches / 1e3
-    nU = rs.num_users // world if world > 1 else rs.num_users
-    nI = rs.num_items // world if world > 1 else rs.num_items
+    nU = n_users // world if world > 1 else n_users
+    nI = n_items // world if world > 1 else n_items
     nbytes, nflops = algorithmic_cost(cls, k, nU, nI, n_local_users // max(1, 1), ldk)
     bound = "mfma" if cls.startswith("gram") and k >= 32 else "hbm"
     if bound == "hbm":
@@ -309,10 +342,14 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32+f64",
-        "data": "synthetic (MovieLens-full shape, seeded; no MovieLens data offline)",
-        "config": {"workload": f"ALS iteration, {args.shape} shape, k={k}, solver={args.solver}",
-                   "k": k, "n_ratings": int(rs.n), "users": int(rs.num_users),
-                   "items": int(rs.num_items), "solver": args.solver,
+        "data": ("synthetic (C5 generator: lognormal activity, rank^-0.9 popularity, uniform "
+                 "half-stars; device-seeded factors)" if c5 else
+                 "synthetic (MovieLens-full shape, seeded; no MovieLens data offline)"),
+        "config": {"workload": (f"ALS iteration, {args.shape} shape"
+                                + (f" x{args.scale:g}" if c5 and args.scale != 1.0 else "")
+                                + f", k={k}, solver={args.solver}"),
+                   "k": k, "n_ratings": int(n_total), "users": int(n_users),
+                   "items": int(n_items), "solver": args.solver,
                    "parallelism": f"shard{world}" if world > 1 else "single"},
         "roofline": {"kernel": cls, "bound": bound, "achieved": round(achieved, 2),
                      "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
@@ -329,7 +366,7 @@ def main():
         "ms_per_step_without_kernel_events": round(plain_ms, 3) if plain_ms else None,
         "replay_cg_identical": replay_identical,
     }
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and not c5:
         try:
             cb = cpu_baseline(args.shape, k, args.cpu_threads, args.cpu_scale)
         except Exception as e:  # the GPU number stands on its own

@@ -115,6 +115,10 @@ void mr_als_destroy(mr_als* ctx);
  * bias), V[num_items*k]; fp64 on the host, fp32 on the device. */
 int mr_als_set_factors(mr_als* ctx, const double* U, const double* V);
 int mr_als_get_factors(mr_als* ctx, double* U, double* V);
+/* Seeded uniform(-1, 1) initial factors generated on the device (the same
+ * values on every rank of a sharded run; not the reference's NumPy RNG
+ * stream).  For workloads whose host tables would be multi-GB (C5). */
+int mr_als_init_factors(mr_als* ctx, unsigned long long seed);
 
 int mr_als_set_solver(mr_als* ctx, int solver, double ridge);
 /* Timing of every kernel launch with HIP events (off by default). */
@@ -125,7 +129,8 @@ int mr_als_set_timing(mr_als* ctx, int enable);
  *                         reference's order, one matvec + update pass
  *   MR_OPT_CG_SPECULATE   1 (default): enqueue CG iteration t+1 before t's
  *                         state is read back when t provably cannot stop
- *                         (ignored in sharded runs); 0: one iteration ahead
+ *                         (decided on exact per-iteration states: identical
+ *                         launches on every rank); 0: one iteration ahead
  *   MR_OPT_WAIT_TIMEOUT_S host wait for a published CG state, seconds
  *                         (default 300; a stalled peer rank then fails the
  *                         call instead of hanging it) */

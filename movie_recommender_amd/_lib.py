@@ -107,6 +107,7 @@ SIGNATURES = {
     "mr_als_half_step": (ctypes.c_int, [VP, ctypes.c_int, DP]),
     "mr_als_work_items": (ctypes.c_longlong, [VP, ctypes.c_int]),
     "mr_als_get_layout": (ctypes.c_int, [VP, ctypes.c_int, LLP, IP, FP, LLP, IP, IP, IP]),
+    "mr_als_init_factors": (ctypes.c_int, [VP, ctypes.c_ulonglong]),
     "mr_als_get_cg_vectors": (ctypes.c_int, [VP, ctypes.c_int, DP, DP, DP]),
     "mr_als_half_step_ex": (ctypes.c_int, [VP, ctypes.c_int, ctypes.c_double, ctypes.c_int, DP]),
     "mr_als_build_normal_equations": (ctypes.c_int, [VP, ctypes.c_int]),

@@ -202,6 +202,19 @@ int mr_als_set_factors(mr_als* ctx, const double* U, const double* V) {
   return guarded([&]() { return ctx->eng.set_factors(U, V); });
 }
 
+int mr_als_init_factors(mr_als* ctx, unsigned long long seed) {
+  MR_CHECK(ctx, "null context");
+  return guarded([&]() -> int {
+    mr::Engine& E = ctx->eng;
+    MR_HIP(hipSetDevice(E.device));
+    if (mr::launch_init_factors(E.stream, E.U, E.k, E.ldk, seed, 0, E.Ufac, E.Ubias) ||
+        mr::launch_init_factors(E.stream, E.I, E.k, E.ldk, seed, 1, E.Vfac, nullptr))
+      return -1;
+    MR_HIP(hipStreamSynchronize(E.stream));
+    return 0;
+  });
+}
+
 int mr_als_get_factors(mr_als* ctx, double* U, double* V) {
   MR_CHECK(ctx, "null context");
   return guarded([&]() { return ctx->eng.get_factors(U, V); });

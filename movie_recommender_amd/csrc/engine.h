@@ -33,6 +33,14 @@ struct Side {
   int64_t n_start_pairs = 0;
 };
 
+// All-gather staging of one factor table (sharded runs, RCCL).
+struct AgStage {
+  int64_t maxrows = 0;                  // rows of the largest shard
+  float *send = nullptr, *recv = nullptr;       // maxrows x ldk, world x maxrows x ldk
+  float *send_b = nullptr, *recv_b = nullptr;   // user bias column
+  int64_t* rb = nullptr;                // device copy of the world+1 row boundaries
+};
+
 struct Pending {
   int cls, tag;
   hipEvent_t a, b;
@@ -72,8 +80,8 @@ struct Engine {
   bool fuse_start = true;   // CG start in the Gram epilogue (MR_OPT_FUSE_START)
   bool speculate = true;    // enqueue CG iteration t+1 before t's state is known
                             // when t provably cannot stop (MR_OPT_CG_SPECULATE;
-                            // never in sharded runs: every rank must issue the
-                            // same collectives)
+                            // decided on exact published states, so every rank
+                            // of a sharded run issues the same launches)
   double wait_timeout_s = 300.0;   // host wait for a published CG state
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
@@ -86,6 +94,7 @@ struct Engine {
   bool has_comm = false;
   mr_comm comm{};
   std::vector<long long> row_begin_u, row_begin_i;
+  AgStage ag_u, ag_i;
 
   ~Engine();
   int init(int dev, int k, int64_t U, int64_t I, int64_t n_u, const int* uv_uid,

@@ -72,6 +72,10 @@ Engine::~Engine() {
     free_side(su, stream);
     free_side(si, stream);
     dfree(Ufac, stream); dfree(Ubias, stream); dfree(Vfac, stream);
+    for (AgStage* A : {&ag_u, &ag_i}) {
+      dfree(A->send, stream); dfree(A->recv, stream); dfree(A->send_b, stream);
+      dfree(A->recv_b, stream); dfree(A->rb, stream);
+    }
     dfree(d_state, stream); dfree(partials, stream); dfree(d_flag, stream);
     (void)hipStreamSynchronize(stream);
     if (h_state) (void)hipHostFree(h_state);
@@ -258,9 +262,9 @@ int Engine::init(int dev, int k_, int64_t U_, int64_t I_, int64_t n_u,
   MR_HIP(hipHostMalloc((void**)&h_state, sizeof(CgState), hipHostMallocDefault));
   MR_HIP(hipHostMalloc((void**)&h_init, sizeof(CgState), hipHostMallocDefault));
   MR_HIP(hipHostMalloc((void**)&h_stage, 64, hipHostMallocDefault));
-  MR_HIP(hipHostMalloc((void**)&h_mirror, sizeof(CgMirror),
+  MR_HIP(hipHostMalloc((void**)&h_mirror, kMirrorSlots * sizeof(CgMirror),
                        hipHostMallocMapped | hipHostMallocCoherent));
-  memset(h_mirror, 0, sizeof(CgMirror));
+  memset(h_mirror, 0, kMirrorSlots * sizeof(CgMirror));
   MR_HIP(hipHostGetDevicePointer((void**)&d_mirror, h_mirror, 0));
   if (dalloc(&d_state, 1, stream) || dalloc(&partials, kMaxParts, stream) ||
       dalloc(&d_flag, 4, stream))
@@ -392,6 +396,27 @@ int Engine::set_rccl(const unsigned char* id, int rank, int world) {
   rccl = (void*)c;
   rccl_world = world;
   rccl_rank = rank;
+  // all-gather staging: every rank's shard padded to the largest one
+  for (int side = 0; side < 2; ++side) {
+    const std::vector<long long>& rb = side == 0 ? row_begin_u : row_begin_i;
+    MR_CHECK((int)rb.size() == world + 1 && rb[0] == 0 && rb[world] == (side == 0 ? U : I),
+             "row boundaries must cover the table");
+    long long mx = 1;
+    for (int r = 0; r < world; ++r) {
+      MR_CHECK(rb[r + 1] >= rb[r], "row boundaries not monotone");
+      mx = std::max(mx, rb[r + 1] - rb[r]);
+    }
+    AgStage& A = side == 0 ? ag_u : ag_i;
+    A.maxrows = mx;
+    if (dalloc(&A.send, mx * ldk, stream) || dalloc(&A.recv, (int64_t)world * mx * ldk, stream) ||
+        dalloc(&A.rb, world + 1, stream))
+      return -1;
+    if (side == 0 &&
+        (dalloc(&A.send_b, mx, stream) || dalloc(&A.recv_b, (int64_t)world * mx, stream)))
+      return -1;
+    std::vector<int64_t> rb64(rb.begin(), rb.end());
+    MR_H2D(A.rb, rb64.data(), rb64.size() * 8, stream);
+  }
   return 0;
 }
 
@@ -413,25 +438,29 @@ int Engine::allreduce_state_slot(int count) {
 }
 
 // Replicate the freshly solved shard rows of a factor table on every rank.
-// RCCL: all-gather-v as one group of in-place broadcasts, rank r the root of
-// rows [row_begin[r], row_begin[r+1]) (fac rows and, for users, the bias).
+// RCCL: ONE ncclAllGather of equal, padded shards (maxrows rows each): the
+// own rows are packed into a send buffer, gathered into world x maxrows rows,
+// and every other rank's rows unpacked into place by one kernel (users: the
+// bias column likewise, a second all-gather of maxrows floats).
 int Engine::allgather_side(bool user) {
   if (!sharded()) return 0;
   const std::vector<long long>& rb = user ? row_begin_u : row_begin_i;
   if (rccl) {
+    AgStage& A = user ? ag_u : ag_i;
     float* fac = user ? Ufac : Vfac;
+    float* bias = user ? Ubias : nullptr;
+    if (launch_pack_rows(stream, rb[rccl_rank], rb[rccl_rank + 1] - rb[rccl_rank], ldk, fac,
+                         bias, A.send, A.send_b))
+      return -1;
     MR_NCCL(ncclGroupStart());
-    for (int r = 0; r < rccl_world; ++r) {
-      const long long n = rb[r + 1] - rb[r];
-      if (n <= 0) continue;
-      MR_NCCL(ncclBroadcast(fac + rb[r] * ldk, fac + rb[r] * ldk, (size_t)(n * ldk), ncclFloat,
-                            r, (ncclComm_t)rccl, stream));
-      if (user)
-        MR_NCCL(ncclBroadcast(Ubias + rb[r], Ubias + rb[r], (size_t)n, ncclFloat, r,
-                              (ncclComm_t)rccl, stream));
-    }
+    MR_NCCL(ncclAllGather(A.send, A.recv, (size_t)(A.maxrows * ldk), ncclFloat,
+                          (ncclComm_t)rccl, stream));
+    if (user)
+      MR_NCCL(ncclAllGather(A.send_b, A.recv_b, (size_t)A.maxrows, ncclFloat, (ncclComm_t)rccl,
+                            stream));
     MR_NCCL(ncclGroupEnd());
-    return 0;
+    return launch_unstage_rows(stream, rccl_world, rccl_rank, A.rb, A.maxrows, ldk, A.recv,
+                               A.recv_b, fac, bias);
   }
   const int64_t rows = user ? U : I;
   // gather [fac | bias] rows through host staging
@@ -470,34 +499,36 @@ int Engine::finalize_sharded(int phase, int seq) {
   return toc(MR_K_CG_CONTROL, -1, a);
 }
 
-// Spin on the host-mapped mirror until a state with seq >= target has been
-// published.  Seqlock protocol (publish(), kernels.hip): the device stores
-// 2 seq - 1 (odd: write in progress), the fields, then 2 seq (release); a
-// copy is accepted only if it was bracketed by the same even value.  Checks
-// the stream for errors and for "stream idle but nothing published" (a bug),
-// and gives up after wait_timeout_s (a stalled peer rank in a sharded run).
+// Spin on the host-mapped mirror ring until the state published under
+// sequence number `target` is in its slot.  Seqlock protocol (publish(),
+// kernels.hip): the device stores 2 seq - 1 (odd: write in progress), the
+// fields, then 2 seq (release); a copy is accepted only if it was bracketed by
+// 2 target.  Checks the stream for errors and for "stream idle but nothing
+// published" (a bug), and gives up after wait_timeout_s (a stalled peer rank
+// in a sharded run).
 int Engine::wait_mirror(int target, CgMirror* out) {
   const int want = 2 * target;
+  CgMirror* slot = h_mirror + (target & (kMirrorSlots - 1));
   long spins = 0;
   const auto t0 = std::chrono::steady_clock::now();
   while (true) {
-    const int s1 = __atomic_load_n(&h_mirror->seq, __ATOMIC_ACQUIRE);
-    if (!(s1 & 1) && s1 >= want) {
+    const int s1 = __atomic_load_n(&slot->seq, __ATOMIC_ACQUIRE);
+    if (s1 == want) {
       CgMirror m;
-      memcpy(&m, (const void*)h_mirror, sizeof(CgMirror));
+      memcpy(&m, (const void*)slot, sizeof(CgMirror));
       __atomic_thread_fence(__ATOMIC_ACQUIRE);
-      if (__atomic_load_n(&h_mirror->seq, __ATOMIC_ACQUIRE) == s1) {
+      if (__atomic_load_n(&slot->seq, __ATOMIC_ACQUIRE) == s1) {
         *out = m;
-        out->seq = s1 / 2;
+        out->seq = target;
         return 0;
       }
-      continue;  // a newer state landed while copying: read again
+      continue;  // overwritten while copying (cannot happen within the ring depth)
     }
+    MR_CHECK(s1 < want, "CG state slot overwritten before it was read");
     if ((++spins & 1023) == 0) {
       const hipError_t q = hipStreamQuery(stream);
       if (q == hipSuccess) {
-        const int s2 = __atomic_load_n(&h_mirror->seq, __ATOMIC_ACQUIRE);
-        if (!(s2 & 1) && s2 >= want) continue;
+        if (__atomic_load_n(&slot->seq, __ATOMIC_ACQUIRE) == want) continue;
         MR_CHECK(false, "CG state was not published (stream idle)");
       }
       MR_CHECK(q == hipErrorNotReady,
@@ -670,34 +701,39 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr, bool start
     return shard ? finalize_sharded(CG_BETA, seq_of.back()) : 0;
   };
 
-  // Iteration 0 cannot stop by stagnation (fails starts at 0) and iteration 1
-  // only after two stagnating steps, so both are enqueued behind the init
-  // without waiting for its state (they are no-ops if the init already
-  // finished the solve: rr < 1e-6 or max_it == 0).
-  // Sharded runs never speculate: a rank's launch count would then depend on
-  // its host's timing, and every launched iteration issues collectives that
-  // must match across ranks.  With one outstanding iteration the launch
-  // sequence is the same on every rank.
-  const int spec = (speculate && !shard) ? 1 : 0;
+  // Host protocol.  Iteration t publishes the state after it (BETA step)
+  // under seq_of[t]; the host always reads the state of an EXACT iteration
+  // (ring slot), so every decision below is a function of states that are
+  // bitwise identical on all ranks of a sharded run (they derive from the
+  // all-reduced scalars): every rank issues the same launches, and with them
+  // the same collectives.  Iteration 0 cannot stop by stagnation (fails
+  // starts at 0), so iterations 0 and 1 are enqueued behind the start without
+  // waiting (no-ops if the start already finished the solve).  Afterwards,
+  // with the exact state S after iteration t known and not done:
+  //   * iteration t+1 is in flight (launched if it was not);
+  //   * iteration t+2 is enqueued too when S proves t+1 cannot stop
+  //     (fails == 0, rr far above 1e-6, t+2 < max_it) -- the stream stays
+  //     busy while the host waits for the state after t+1;
+  //   * iteration t+1 publishes (S not done => it is not a no-op).
+  const int spec = speculate ? 1 : 0;
   int launched = 0;          // iterations enqueued so far
   for (; launched < std::min(spec ? 2 : 1, max_it); ++launched)
     if (launch_iter(launched)) return -1;
   CgMirror ms{};
   if (wait_mirror(seq_init, &ms)) return -1;
-  int known = -1;            // index of the last iteration whose state is in ms
+  int known = -1;            // ms = exact state after iteration `known` (-1: the start)
   while (!ms.done) {
-    if (launched <= known + 1) {
+    if (launched == known + 1) {
       if (launch_iter(launched)) return -1;
       ++launched;
     }
-    // speculate one further iteration when iteration known+1 cannot stop
     if (spec && launched == known + 2 && ms.fails == 0 && ms.rr > 1e-4 && known + 2 < max_it) {
       if (launch_iter(launched)) return -1;
       ++launched;
     }
     if (wait_mirror(seq_of[known + 1], &ms)) return -1;
-    while (known + 1 < (int)seq_of.size() && seq_of[known + 1] <= ms.seq) ++known;
-    MR_CHECK(launched <= max_it + 2, "CG did not terminate");
+    ++known;
+    MR_CHECK(known <= max_it, "CG did not terminate");
   }
   for (size_t i = pend0; i < pending.size(); ++i) pending[i].n_real = ms.n_matvec;
   if (final_rr) *final_rr = ms.final_rr;

@@ -1034,10 +1034,12 @@ __device__ __forceinline__ void store_state(CgState* st, const CgScalars& v) {
   ast(&st->sharded, v.sharded);
 }
 
-// Seqlock publish into the host-mapped mirror (Engine::wait_mirror): odd
-// 2 seq - 1 marks a write in progress, the even 2 seq (release) its end.
-__device__ __forceinline__ void publish(const CgScalars& v, CgMirror* m, int seq) {
-  if (!m) return;
+// Seqlock publish into slot seq % kMirrorSlots of the host-mapped mirror ring
+// (Engine::wait_mirror): odd 2 seq - 1 marks a write in progress, the even
+// 2 seq (release) its end.
+__device__ __forceinline__ void publish(const CgScalars& v, CgMirror* ring, int seq) {
+  if (!ring) return;
+  CgMirror* m = ring + (seq & (kMirrorSlots - 1));
   __hip_atomic_store(&m->seq, 2 * seq - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __threadfence_system();
   m->done = v.done;
@@ -1614,6 +1616,87 @@ __global__ void predict_kernel(int64_t n, int k, int ldk, const int* __restrict_
     for (int j = 0; j < k; ++j) s += (double)Uf[u * ldk + j] * Vf[i * ldk + j];
     out[t] = s + Ub[u];
   }
+}
+
+__global__ void pack_rows_kernel(int64_t n4, int ldk4, const float4* __restrict__ fac,
+                                 const float* __restrict__ bias, float4* __restrict__ send,
+                                 float* __restrict__ send_b) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n4;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    send[t] = fac[t];
+    if (bias && t % ldk4 == 0) send_b[t / ldk4] = bias[t / ldk4];
+  }
+}
+
+int launch_pack_rows(hipStream_t s, int64_t r0, int64_t n, int ldk, const float* fac,
+                     const float* bias, float* send, float* send_b) {
+  if (n <= 0) return 0;
+  const int ldk4 = ldk / 4;
+  pack_rows_kernel<<<grid_for(n * ldk4), 256, 0, s>>>(
+      n * ldk4, ldk4, reinterpret_cast<const float4*>(fac + r0 * ldk), bias ? bias + r0 : nullptr,
+      reinterpret_cast<float4*>(send), send_b);
+  MR_HIP(hipGetLastError());
+  return 0;
+}
+
+__global__ void unstage_rows_kernel(int world, int skip, const int64_t* __restrict__ rb,
+                                    int64_t maxrows, int ldk4, const float4* __restrict__ recv,
+                                    const float* __restrict__ recv_b, float4* __restrict__ fac,
+                                    float* __restrict__ bias) {
+  const int64_t per = maxrows * ldk4;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < (int64_t)world * per;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(t / per);
+    const int64_t rem = t - (int64_t)r * per;
+    const int64_t j = rem / ldk4;
+    if (r == skip || j >= rb[r + 1] - rb[r]) continue;
+    const int c = (int)(rem - j * ldk4);
+    fac[(rb[r] + j) * ldk4 + c] = recv[t];
+    if (bias && c == 0) bias[rb[r] + j] = recv_b[(int64_t)r * maxrows + j];
+  }
+}
+
+int launch_unstage_rows(hipStream_t s, int world, int skip, const int64_t* rb,
+                        int64_t maxrows, int ldk, const float* recv, const float* recv_b,
+                        float* fac, float* bias) {
+  const int ldk4 = ldk / 4;
+  unstage_rows_kernel<<<grid_for((int64_t)world * maxrows * ldk4), 256, 0, s>>>(
+      world, skip, rb, maxrows, ldk4, reinterpret_cast<const float4*>(recv), recv_b,
+      reinterpret_cast<float4*>(fac), bias);
+  MR_HIP(hipGetLastError());
+  return 0;
+}
+
+// Seeded uniform(-1, 1) factors generated on the device (splitmix64 of the
+// (table, row, column) index): identical on every rank, no host table
+// (multi-GB at C5).  Padding columns stay 0.
+__device__ __forceinline__ double unit_hash(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return (double)(x >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0;
+}
+
+__global__ void init_factors_kernel(int64_t rows, int k, int ldk, uint64_t seed, int table,
+                                    float* __restrict__ fac, float* __restrict__ bias) {
+  const int64_t n = rows * ldk;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = t / ldk;
+    const int c = (int)(t - r * ldk);
+    const uint64_t base = (seed * 0x100000001B3ull) ^ ((uint64_t)table << 60);
+    fac[t] = c < k ? (float)unit_hash(base + (uint64_t)r * (k + 1) + c) : 0.f;
+    if (bias && c == 0) bias[r] = (float)unit_hash(base + (uint64_t)r * (k + 1) + k);
+  }
+}
+
+int launch_init_factors(hipStream_t s, int64_t rows, int k, int ldk, uint64_t seed, int table,
+                        float* fac, float* bias) {
+  if (rows <= 0) return 0;
+  init_factors_kernel<<<grid_for(rows * ldk), 256, 0, s>>>(rows, k, ldk, seed, table, fac, bias);
+  MR_HIP(hipGetLastError());
+  return 0;
 }
 
 int launch_x_to_vec(hipStream_t s, int64_t n, int64_t nb, const float* x, const float* xb,

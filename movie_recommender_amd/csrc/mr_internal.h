@@ -188,9 +188,12 @@ struct CgState {
   int32_t sharded;  // 1: the last block only sums into comm[0] for the all-reduce
 };
 
-// Host-visible copy of the CG state, written by cg_control into pinned,
-// host-mapped coherent memory after every INIT/BETA step (seq last, with a
-// system-scope release), so the host can poll it without a stream sync.
+// Host-visible copies of the CG state: a ring of kMirrorSlots records in
+// pinned, host-mapped coherent memory.  Every INIT / BETA step publishes its
+// state under a sequence number into slot seq % kMirrorSlots (seqlock: odd
+// while being written), so the host reads the state of an EXACT iteration --
+// what makes launch decisions identical on every rank of a sharded run.
+constexpr int kMirrorSlots = 8;
 struct CgMirror {
   int32_t seq;
   int32_t done;
@@ -256,6 +259,18 @@ int launch_unpack_factors(hipStream_t s, int64_t rows, int width, int k,
                           int ldk, const double* src, float* fac, float* bias);
 int launch_pack_factors(hipStream_t s, int64_t rows, int width, int k, int ldk,
                         const float* fac, const float* bias, double* dst);
+// Sharded all-gather staging: pack rows [r0, r0+n) of fac (and bias) into
+// send; unstage world x maxrows gathered rows into their table rows
+// (rb[s] .. rb[s+1]) for every rank s != skip.
+int launch_pack_rows(hipStream_t s, int64_t r0, int64_t n, int ldk, const float* fac,
+                     const float* bias, float* send, float* send_b);
+int launch_unstage_rows(hipStream_t s, int world, int skip, const int64_t* rb,
+                        int64_t maxrows, int ldk, const float* recv, const float* recv_b,
+                        float* fac, float* bias);
+// Seeded uniform(-1, 1) factor table on the device (table 0: U with bias,
+// 1: V); the same values on every rank.
+int launch_init_factors(hipStream_t s, int64_t rows, int k, int ldk, uint64_t seed, int table,
+                        float* fac, float* bias);
 int launch_predict(hipStream_t s, int64_t n, int k, int ldk, const int* uid,
                    const int* iid, const float* Ufac, const float* Ubias,
                    const float* Vfac, double* out);

@@ -1,4 +1,4 @@
-"""Sharded ALS: one process per GPU, users and movies partitioned by rating count.
+"""Sharded ALS: one process per GPU, users and movies partitioned by per-step cost.
 
 Replaces the *role* of the reference's process fan-out
 (``python/full_data/cluster_server.py`` / ``worker_server.py`` and the
@@ -6,12 +6,14 @@ multiprocessing pipes of ``movie_lens_data_proc.py``), which the reference
 uses for evaluation, never for the ALS solve.  Here the solve itself shards:
 
 * rank r owns users ``[ub[r], ub[r+1])`` and items ``[ib[r], ib[r+1])``;
-  boundaries balance the rating count (``shard_bounds``);
+  boundaries balance the per-step cost ``n_e + C(k)`` of each entity
+  (``entity_cost``: the Gram's work is per rating, the CG's per entity);
 * each rank builds its users' normal equations from a full replica of V and
   its items' from a full replica of U, so no rating crosses ranks;
 * the reference's global CG scalars (``matrix.cpp:485, 497, 507``) are
   all-reduced (2 doubles per CG iteration) and the freshly solved factor
-  shard is all-gathered after every half-step.
+  shard is all-gathered after every half-step (RCCL: one ncclAllGather of
+  equal padded shards).
 
 The collectives are supplied through ``mr_comm`` callbacks backed by
 ``torch.distributed`` (``nccl`` = RCCL over xGMI on MI355X, or ``gloo``).
@@ -37,12 +39,28 @@ def shard_bounds(counts, world):
     return b
 
 
-def shard_views(user_ids, item_ids, ratings, num_users, num_items, rank, world):
-    """(user_range, item_range, user_view, item_view, ub, ib) for ``rank``."""
+def entity_cost(counts, k, cg_iterations=6):
+    """Per-step cost of each entity in rating units: its ratings (the Gram
+    gathers a 4k-byte row per rating) plus ``cg_iterations`` block-GEMV
+    passes over its normal equations and fp64 CG vectors (4 gsize(k) + 40
+    (ldk + 1) bytes each, the CG's cost is per entity, not per rating)."""
+    counts = np.asarray(counts, np.int64)
+    if k is None:
+        return counts
+    nb = (k + 15) // 16
+    gsize = (nb * (nb - 1) // 2 + nb // 2 + nb % 2) * 256 + (nb // 2) * 16
+    ldk = nb * 16
+    c = int(round(cg_iterations * (4 * gsize + 40 * (ldk + 1)) / (4 * k + 8)))
+    return counts + c
+
+
+def shard_views(user_ids, item_ids, ratings, num_users, num_items, rank, world, k=None):
+    """(user_range, item_range, user_view, item_view, ub, ib) for ``rank``;
+    with ``k`` the boundaries balance ``entity_cost``, else rating counts."""
     uc = np.bincount(user_ids, minlength=num_users)
     ic = np.bincount(item_ids, minlength=num_items)
-    ub = shard_bounds(uc, world)
-    ib = shard_bounds(ic, world)
+    ub = shard_bounds(entity_cost(uc, k), world)
+    ib = shard_bounds(entity_cost(ic, k), world)
     u0, u1 = int(ub[rank]), int(ub[rank + 1])
     i0, i1 = int(ib[rank]), int(ib[rank + 1])
     su = (user_ids >= u0) & (user_ids < u1)
@@ -136,7 +154,7 @@ def sharded_context(user_ids, item_ids, ratings, k, num_users, num_items, device
     from .engine import AlsContext
     rank, world = dist.get_rank(), dist.get_world_size()
     (u0, u1), (i0, i1), uv, iv, ub, ib = shard_views(
-        user_ids, item_ids, ratings, num_users, num_items, rank, world)
+        user_ids, item_ids, ratings, num_users, num_items, rank, world, k=k)
     ctx = AlsContext(uv[0], uv[1], uv[2], k, num_users, num_items, device=device,
                      user_range=(u0, u1), item_range=(i0, i1), item_view=iv, **kw)
     if comm == "rccl":

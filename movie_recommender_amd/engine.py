@@ -121,6 +121,10 @@ class AlsContext:
                                                  V.ctypes.data_as(_lib.DP)),
                    "mr_als_set_factors")
 
+    def init_factors(self, seed=0):
+        """Seeded uniform(-1, 1) factors generated on the device."""
+        _lib.check(_lib.lib().mr_als_init_factors(self._h, int(seed)), "mr_als_init_factors")
+
     def get_factors(self):
         U = np.empty(self.num_users * (self.k + 1))
         V = np.empty(self.num_items * self.k)

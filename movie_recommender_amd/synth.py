@@ -169,3 +169,84 @@ def dense_fixture(num_users, num_items, k, keep=0.8, seed=7, noise=0.1):
     n = int(np.ceil(len(uu) * keep))
     a, b = perm[:n], perm[n:]
     return uu[a], ii[a], r[a], uu[b], ii[b], r[b]
+
+
+# ---------------------------------------------------------------------------
+# C5: synthetic 10 M users x 1 M items x 1e9 ratings (SURVEY.md 8, configs[4])
+# ---------------------------------------------------------------------------
+C5_SHAPE = (10_000_000, 1_000_000, 1_000_000_000)
+
+
+class C5Generator:
+    """Streamed generator of the C5 roofline workload, never materialised
+    whole on one host.  User activity ~ LogNormal(0, 1.2) fixes every user's
+    degree up front (rounded, >= 1); item popularity ~ rank^-0.9 over
+    shuffled ranks, drawn through a 2^24-entry inverse-CDF table; ratings are
+    uniform half-stars minus 3.0 (rating - median).  Users are generated in
+    blocks of ``block`` with their own seeded streams, so any rank can
+    regenerate any block: a rank's user view is its own blocks, its item view
+    a filtered pass over all blocks.  Duplicate (user, item) pairs are kept
+    (the reference treats them as separate ratings) and there is no degree
+    shrink (the reference's k+1 / k rule is MovieLens preparation; here users
+    with fewer ratings than unknowns simply give singular blocks, which CG
+    handles as the reference's CG does)."""
+
+    LUT_BITS = 24
+
+    def __init__(self, scale=1.0, seed=DATA_SEED, block=1 << 16, shape=C5_SHAPE):
+        nu, ni, nr = shape
+        self.num_users = max(1, int(nu * scale))
+        self.num_items = max(1, int(ni * scale))
+        n_target = max(1, int(nr * scale))
+        self.seed = seed
+        self.block = block
+        rng = np.random.default_rng(seed)
+        act = rng.lognormal(0.0, 1.2, self.num_users)
+        self.deg = np.maximum(1, np.rint(act * (n_target / act.sum()))).astype(np.int64)
+        self.off = np.zeros(self.num_users + 1, np.int64)
+        np.cumsum(self.deg, out=self.off[1:])
+        self.n = int(self.off[-1])
+        pop = (rng.permutation(self.num_items) + 1.0) ** -0.9
+        self.p_item = pop / pop.sum()
+        cdf = np.cumsum(self.p_item)
+        T = 1 << self.LUT_BITS
+        self.lut = np.minimum(np.searchsorted(cdf, (np.arange(T) + 0.5) / T, side="right"),
+                              self.num_items - 1).astype(np.int32)
+
+    @property
+    def n_blocks(self):
+        return (self.num_users + self.block - 1) // self.block
+
+    def gen_block(self, b):
+        """(user ids, item ids, ratings) of users [b*block, (b+1)*block)."""
+        u0 = b * self.block
+        u1 = min(self.num_users, u0 + self.block)
+        n = int(self.off[u1] - self.off[u0])
+        rng = np.random.default_rng([self.seed, 5, b])
+        uid = np.repeat(np.arange(u0, u1, dtype=np.int32), self.deg[u0:u1])
+        iid = self.lut[rng.integers(0, 1 << self.LUT_BITS, n)]
+        r = rng.integers(1, 11, n) / 2.0 - 3.0
+        return uid, iid, r
+
+    def expected_item_counts(self):
+        return self.p_item * self.n
+
+    def user_view(self, u0, u1):
+        parts = [self.gen_block(b) for b in range(u0 // self.block,
+                                                   (u1 + self.block - 1) // self.block)]
+        uid, iid, r = (np.concatenate(x) for x in zip(*parts)) if parts else \
+            (np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(0))
+        sel = (uid >= u0) & (uid < u1)
+        return uid[sel], iid[sel], r[sel]
+
+    def item_view(self, i0, i1):
+        us, is_, rs = [], [], []
+        for b in range(self.n_blocks):
+            uid, iid, r = self.gen_block(b)
+            sel = (iid >= i0) & (iid < i1)
+            us.append(uid[sel]); is_.append(iid[sel]); rs.append(r[sel])
+        return np.concatenate(us), np.concatenate(is_), np.concatenate(rs)
+
+    def all_ratings(self):
+        parts = [self.gen_block(b) for b in range(self.n_blocks)]
+        return tuple(np.concatenate(x) for x in zip(*parts))

@@ -48,6 +48,21 @@ def test_shard_bounds_balanced_and_complete():
         assert max(load) <= counts.sum() / world + counts.max()
 
 
+def test_entity_cost_balances_gram_and_cg_work():
+    """Light entities cost a CG pass each: with the per-entity term the
+    rank holding many light users gets fewer of them than a pure rating
+    balance would give it."""
+    from movie_recommender_amd.distributed import entity_cost, shard_bounds
+    counts = np.concatenate([np.full(1000, 500), np.full(20000, 25)])   # heavy then light
+    plain = shard_bounds(counts, 2)
+    cost = entity_cost(counts, 64)
+    assert np.all(cost - counts == cost[0] - counts[0]) and cost[0] - counts[0] > 100
+    b = shard_bounds(cost, 2)
+    assert b[1] > plain[1]                 # the heavy rank takes some light users
+    load = [cost[b[r]:b[r + 1]].sum() for r in range(2)]
+    assert abs(load[0] - load[1]) <= cost.max()
+
+
 def test_shard_views_partition_every_rating():
     from movie_recommender_amd.distributed import shard_views
     d = load_golden("als_mlshape_k10_it2.npz")
@@ -64,7 +79,8 @@ def test_shard_views_partition_every_rating():
 
 
 @pytest.mark.parametrize("fixture,max_it", [("als_dense_300x200_k10.npz", 200),
-                                            ("als_mlshape_k10_it4.npz", 4)])
+                                            ("als_mlshape_k10_it4.npz", 4),
+                                            ("als_mlshape_k64_it2.npz", 2)])
 def test_sharded_algorithm_gloo_cpu(tmp_path, fixture, max_it):
     """World size 2 on CPU: sharded normal equations + all-reduced CG scalars +
     all-gathered shards reproduce the single-process algorithm (and the
@@ -84,14 +100,20 @@ def test_sharded_algorithm_gloo_cpu(tmp_path, fixture, max_it):
 
 
 @pytest.mark.gpu
-def test_engine_two_ranks_gloo_matches_single(gpu, tmp_path):
+@pytest.mark.parametrize("fixture,max_it", [("als_dense_300x200_k10.npz", 200),
+                                            ("als_dense_300x260_k64.npz", 200),
+                                            ("als_mlshape_k64_it4.npz", 4)])
+def test_engine_two_ranks_gloo_matches_single(gpu, tmp_path, fixture, max_it):
+    """The real engine sharded over 2 ranks (both on cuda:0 on a one-GPU box;
+    cost-balanced shards, all-reduced CG scalars, all-gathered factor shards)
+    against the single-context run and the compiled reference's golden."""
     from movie_recommender_amd.engine import AlsContext
-    fixture = "als_dense_300x200_k10.npz"
     d = load_golden(fixture)
-    U, V, ret = run_workers("engine_gloo", fixture, 2, tmp_path)
-    with AlsContext(d["user_ids"], d["item_ids"], d["ratings"], 10, 300, 200) as ctx:
+    k, nU, nI = int(d["k"]), int(d["num_users"]), int(d["num_items"])
+    U, V, ret = run_workers("engine_gloo", fixture, 2, tmp_path, max_it)
+    with AlsContext(d["user_ids"], d["item_ids"], d["ratings"], k, nU, nI) as ctx:
         ctx.set_factors(d["U0"], d["V0"])
-        ret1 = ctx.run()
+        ret1 = ctx.run(0.01, max_it)
         U1, V1 = ctx.get_factors()
     assert ret == ret1 == int(d["ret"])
     assert rel_err(U, U1) < 1e-5 and rel_err(V, V1) < 1e-5
