@@ -91,14 +91,18 @@ struct MvScratch {
 };
 
 // y = G_e v for ONE entity, by one wave, on tri16 tiles already in registers
-// (lane l holds float4 l of every tile: T[l>>2][4(l&3) .. +3]).  Lane l
-// accumulates the row product T v_bj into y_bi and, for bi < bj, the column
-// product T^T v_bi into y_bj (fp64); the 4-lane row partials are summed by DPP
-// inside each quad, the 16-lane column partials through LDS, both in a fixed
-// order.  Requires sc.pv (v in virtual order) and sc.dd staged.  Returns y at
+// (lane l holds float4 l of every tile: T[l>>2][4(l&3) .. +3]).  Row products
+// T v_bj go to y_bi, and for bi < bj column products T^T v_bi to y_bj, all in
+// fp64.  Two passes with one block's accumulators live at a time -- block
+// rows (summed over the 4 lanes of a row by DPP), then block columns (the
+// 16-lane column partials through LDS) -- and a sched_barrier per tile, so the
+// fp64 copies of the tiles are not all hoisted: the kernel fits 4 waves per
+// SIMD.  Requires sc.pv (v in virtual order) and sc.dd staged.  Returns y at
 // virtual index lane + 64 h in yo[h] (0 for padding, n >= k) and, user side,
-// the bias row yb = Gs.v + Gn vb (wave-uniform); Gs_e / gn are the entity's row
-// sums and count.  The user-side bias column Gs vb is added to every y.
+// the bias row yb = Gs.v + Gn vb (wave-uniform); Gs_e / gn are the entity's
+// row sums and count.  The user-side bias column Gs vb is added to every y.
+// A diagonal block contributes only its stored triangle (the bf16x3 MFMA sum
+// is not bitwise symmetric; mr_internal.h).
 template <int NB, bool USER>
 __device__ __forceinline__ void tile_matvec(
     const float4 (&g)[NB * (NB - 1) / 2 + NB / 2 + (NB & 1)], MvScratch<NB>& sc, double vb,
@@ -108,80 +112,74 @@ __device__ __forceinline__ void tile_matvec(
   constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
   const int lane = threadIdx.x & 63;
   const int rr = lane >> 2, c4 = (lane & 3) * 4;
-  double accR[NB];
-  double accC[NB][4];
-#pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    accR[b] = 0.0;
-#pragma unroll
-    for (int x = 0; x < 4; ++x) accC[b][x] = 0.0;
-  }
-  // strictly-upper tiles: row product into y_bi, column product into y_bj
-  int t = 0;
+  auto tile = [&](int t, double (&ge)[4]) {
+    const float4 gg = g[t];
+    ge[0] = gg.x; ge[1] = gg.y; ge[2] = gg.z; ge[3] = gg.w;
+  };
+  // diagonal tile of block b and whether its stored triangle is the lower one
+  auto diag_tile = [&](int b, bool& lower) {
+    lower = (b & 1) && b < 2 * NF;
+    return (b < 2 * NF) ? NO + (b >> 1) : NO + NF;
+  };
+  // pass 1: block rows, y_bi[rr] = sum_bj T(bi,bj)[rr][:] v_bj
 #pragma unroll
   for (int bi = 0; bi < NB; ++bi) {
-    const double pi = sc.pv[16 * bi + rr];
+    double s0 = 0.0;
 #pragma unroll
     for (int bj = bi + 1; bj < NB; ++bj) {
-      const float4 gg = g[t];
-      const double ge[4] = {gg.x, gg.y, gg.z, gg.w};
-      const double2 pa = *reinterpret_cast<const double2*>(&sc.pv[16 * bj + c4]);
-      const double2 pb = *reinterpret_cast<const double2*>(&sc.pv[16 * bj + c4 + 2]);
-      double s0 = accR[bi];
-      s0 = fma(ge[0], pa.x, s0);
-      s0 = fma(ge[1], pa.y, s0);
-      s0 = fma(ge[2], pb.x, s0);
-      s0 = fma(ge[3], pb.y, s0);
-      accR[bi] = s0;
+      double ge[4];
+      tile(off_index(bi, bj, NB), ge);
 #pragma unroll
-      for (int x = 0; x < 4; ++x) accC[bj][x] = fma(ge[x], pi, accC[bj][x]);
-      ++t;
+      for (int x = 0; x < 4; ++x) s0 = fma(ge[x], sc.pv[16 * bj + c4 + x], s0);
+      __builtin_amdgcn_sched_barrier(0);
     }
-  }
-  // folded diagonal tiles: c >= r belongs to D_2m (row; column also for
-  // c > r), c < r to D_2m+1 (row and column)
+    {
+      bool lower;
+      const int t = diag_tile(bi, lower);
+      double ge[4];
+      tile(t, ge);
 #pragma unroll
-  for (int m = 0; m < NF; ++m) {
-    const int b0 = 2 * m, b1 = 2 * m + 1;
-    const float4 gg = g[NO + m];
-    const double ge[4] = {gg.x, gg.y, gg.z, gg.w};
-    const double pr0 = sc.pv[16 * b0 + rr], pr1 = sc.pv[16 * b1 + rr];
-#pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      const int c = c4 + x;
-      const double gu = (c >= rr) ? ge[x] : 0.0;
-      const double gc = (c > rr) ? ge[x] : 0.0;
-      const double gl = (c < rr) ? ge[x] : 0.0;
-      accR[b0] = fma(gu, sc.pv[16 * b0 + c], accR[b0]);
-      accR[b1] = fma(gl, sc.pv[16 * b1 + c], accR[b1]);
-      accC[b0][x] = fma(gc, pr0, accC[b0][x]);
-      accC[b1][x] = fma(gl, pr1, accC[b1][x]);
+      for (int x = 0; x < 4; ++x) {
+        const int c = c4 + x;
+        const bool use = lower ? (c < rr) : (c >= rr);   // lower: diagonal from dd
+        s0 = fma(use ? ge[x] : 0.0, sc.pv[16 * bi + c], s0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
+    const double rs = quad_sum_f64(s0);
+    if ((lane & 3) == 0) sc.redR[bi][rr] = rs;
   }
-  if constexpr ((NB & 1) != 0) {
-    // last diagonal block, stored full: only its upper triangle defines G
-    // (the bf16x3 MFMA sum is not bitwise symmetric: B[i][j] and B[j][i] add
-    // the hm / mh products in opposite orders), as in packed_offset
-    const int b0 = NB - 1;
-    const float4 gg = g[NO + NF];
-    const double ge[4] = {gg.x, gg.y, gg.z, gg.w};
-    const double pr0 = sc.pv[16 * b0 + rr];
+  // pass 2: block columns, y_bj[c] += sum_{bi <= bj} T(bi,bj)[:][c] v_bi
+  // (16-lane partials per column through LDS)
 #pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      const int c = c4 + x;
-      const double gu = (c >= rr) ? ge[x] : 0.0;
-      const double gc = (c > rr) ? ge[x] : 0.0;
-      accR[b0] = fma(gu, sc.pv[16 * b0 + c], accR[b0]);
-      accC[b0][x] = fma(gc, pr0, accC[b0][x]);
+  for (int bj = 0; bj < NB; ++bj) {
+    double cc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int bi = 0; bi < bj; ++bi) {
+      double ge[4];
+      tile(off_index(bi, bj, NB), ge);
+      const double pi = sc.pv[16 * bi + rr];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) cc[x] = fma(ge[x], pi, cc[x]);
+      __builtin_amdgcn_sched_barrier(0);
     }
-  }
+    {
+      bool lower;
+      const int t = diag_tile(bj, lower);
+      double ge[4];
+      tile(t, ge);
+      const double pr = sc.pv[16 * bj + rr];
 #pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    const double rs = quad_sum_f64(accR[b]);
-    if ((lane & 3) == 0) sc.redR[b][rr] = rs;
-    double2* dst = reinterpret_cast<double2*>(&sc.redC[b][4 * lane]);
-    dst[0] = make_double2(accC[b][0], accC[b][1]);
-    dst[1] = make_double2(accC[b][2], accC[b][3]);
+      for (int x = 0; x < 4; ++x) {
+        const int c = c4 + x;
+        const bool use = lower ? (c < rr) : (c > rr);
+        cc[x] = fma(use ? ge[x] : 0.0, pr, cc[x]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    double2* dst = reinterpret_cast<double2*>(&sc.redC[bj][4 * lane]);
+    dst[0] = make_double2(cc[0], cc[1]);
+    dst[1] = make_double2(cc[2], cc[3]);
   }
   __builtin_amdgcn_wave_barrier();
   double ybp = 0.0;
@@ -776,6 +774,9 @@ __device__ __forceinline__ void gram_wave(
   // tri16 layout (mr_internal.h): off-diagonal blocks as full tiles, diagonal
   // blocks folded pairwise; every store index is compile-time except the lane
   constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2, NTILE = NO + NF + (NB & 1);
+  // (plain stores: 4-byte sc1 write-through stores, to keep the gathered rows
+  // in L2, made the kernel 4 % slower -- users 884 -> 924 us)
+  auto st = [&](int64_t off, float v) { Gd[off] = v; };
   int t = 0;
 #pragma unroll
   for (int bi = 0; bi < NB; ++bi) {
@@ -786,14 +787,14 @@ __device__ __forceinline__ void gram_wave(
         const int row = 4 * q + r;
         const float v = acc[t][r];
         if (bi != bj) {
-          Gd[off_index(bi, bj, NB) * 256 + row * 16 + col] = v;
+          st(off_index(bi, bj, NB) * 256 + row * 16 + col, v);
         } else if ((NB & 1) && bi == NB - 1) {
-          Gd[(NO + NF) * 256 + row * 16 + col] = v;
+          st((NO + NF) * 256 + row * 16 + col, v);
         } else if ((bi & 1) == 0) {
-          if (col >= row) Gd[(NO + (bi >> 1)) * 256 + row * 16 + col] = v;
+          if (col >= row) st((NO + (bi >> 1)) * 256 + row * 16 + col, v);
         } else {
-          if (col < row) Gd[(NO + (bi >> 1)) * 256 + row * 16 + col] = v;
-          else if (col == row) Gd[NTILE * 256 + (bi >> 1) * 16 + row] = v;
+          if (col < row) st((NO + (bi >> 1)) * 256 + row * 16 + col, v);
+          else if (col == row) st(NTILE * 256 + (bi >> 1) * 16 + row, v);
         }
       }
       ++t;
@@ -1137,7 +1138,7 @@ __device__ void last_block_finalize(CgState* st, int phase, double* partials, Cg
 // users 225 -> 195 us, items 103 -> 94 us, and the CG update 28 -> 25 us
 // because its vectors stay cached).
 template <int NB, bool USER>
-__global__ __launch_bounds__(256) void cg_matvec_kernel(
+__global__ __launch_bounds__(256, (NB <= 4 ? 4 : 1)) void cg_matvec_kernel(
     const CgState* __restrict__ st, int update_p, int64_t E, int k, int ldk,
     const float* __restrict__ G, const float* __restrict__ Gs,
     const float* __restrict__ Gn, double* __restrict__ v, double* __restrict__ vb,
