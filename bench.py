@@ -158,6 +158,8 @@ def main():
     ap.add_argument("--solver", default="cg", choices=["cg", "cholesky"])
     ap.add_argument("--ridge", type=float, default=0.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-fuse-start", action="store_true",
+                    help="start CG with a matvec + update pass instead of the Gram epilogue")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="time steps without per-launch HIP events (no roofline)")
     ap.add_argument("--cpu-scale", type=float, default=0.25)
@@ -230,6 +232,8 @@ def main():
             ctx = AlsContext(rs.user_ids, rs.item_ids, rs.ratings, k, n_users, n_items,
                              device=local_rank, solver=args.solver, ridge=args.ridge)
         ctx.set_factors(U0, V0)
+    if args.no_fuse_start:
+        ctx.set_option("fuse_start", 0)
     ctx.sync()
     log(f"[bench] context built in {time.perf_counter() - t0:.2f} s")
 
@@ -301,7 +305,7 @@ def main():
     avg_s = tot_ms / launches / 1e3
     nU = n_users // world if world > 1 else n_users
     nI = n_items // world if world > 1 else n_items
-    nbytes, nflops = algorithmic_cost(cls, k, nU, nI, n_local_users // max(1, 1), ldk)
+    nbytes, nflops = algorithmic_cost(cls, k, nU, nI, n_local_users, ldk, not args.no_fuse_start)
     bound = "mfma" if cls.startswith("gram") and k >= 32 else "hbm"
     if bound == "hbm":
         achieved, peak, unit = nbytes / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
@@ -324,7 +328,7 @@ def main():
     for c, ms in st["kernel_ms"].items():
         n = st["kernel_launches"][c]
         if n:
-            b, fl = algorithmic_cost(c, k, nU, nI, n_local_users, ldk)
+            b, fl = algorithmic_cost(c, k, nU, nI, n_local_users, ldk, not args.no_fuse_start)
             kernel_table[c] = {"total_ms": round(ms, 3), "launches": n,
                                "avg_us": round(ms / n * 1e3, 2),
                                "alg_GBps": round(b / (ms / n / 1e3) / 1e9, 1) if b else None,

@@ -346,7 +346,7 @@ __device__ __forceinline__ void load_row_seg(float (&v)[NB], const float* __rest
 template <int NB>
 struct StartScratch {
   double pv[16 * NB];                // the vector, virtual order
-  double yR[16 * NB];                // row-product sums
+  double partR[4 * NB][64];          // [4 bi + r][lane]: row-product partials
   double yC[16 * NB];                // column-product sums
   float sC[16 * NB];                 // rhs c, virtual order
   float sGs[16 * NB];                // user side: row sums, virtual order
@@ -360,9 +360,10 @@ __host__ __device__ constexpr int acc_tile(int bi, int bj, int nb) {
 // y = G v straight from the MFMA accumulators of the Gram wave (no memory
 // round trip), products accumulated in fp64.  acc[t(bi,bj)] (bi <= bj,
 // diagonal blocks FULL) holds B[4q + r][col] in lane (q, col).  Row products
-// B v_bj go to y_bi (summed over the 16 lanes of row q by DPP), column
-// products B^T v_bi to y_bj (summed over the 4 rows by lane shuffles), both
-// in a fixed order; a diagonal block contributes its stored triangle only.
+// B v_bj go to y_bi (per-lane partials summed over the 16 lanes of row q
+// through LDS -- a DPP tree cost 4x the instructions), column products
+// B^T v_bi to y_bj (summed over the 4 rows by lane shuffles), both in a
+// fixed order; a diagonal block contributes its stored triangle only.
 // Two passes (block rows, then block columns) with one tile's fp64 copy live
 // at a time: this epilogue must fit the main loop's register budget (3 waves
 // per SIMD at k = 64), so tile conversions are not hoisted
@@ -395,11 +396,7 @@ __device__ __forceinline__ void acc_matvec(const floatx4 (&acc)[NB * (NB + 1) / 
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const double rs = row_sum_f64(R[r]);
-      // lanes 0..3 of row q hold identical row sums: lane (q, r) stores row 4q + r
-      if (col == r) sc.yR[16 * bi + 4 * q + r] = rs;
-    }
+    for (int r = 0; r < 4; ++r) sc.partR[4 * bi + r][lane] = R[r];
   }
   // pass 2: column products y_bj[col] = sum_{bi <= bj} B(bi,bj)[:][col] . v_bi
 #pragma unroll
@@ -430,7 +427,17 @@ __device__ __forceinline__ void acc_matvec(const floatx4 (&acc)[NB * (NB + 1) / 
     const int o = lane + 64 * h;
     yo[h] = 0.0;
     if (o >= NP || nat_of(o, NB) >= k) continue;
-    yo[h] = sc.yR[o] + sc.yC[o];
+    // row 4q + r of block b: the 16 lanes (q, 0..15) of partial r
+    const int b = o >> 4, i = o & 15;
+    const double2* pr = reinterpret_cast<const double2*>(&sc.partR[4 * b + (i & 3)][16 * (i >> 2)]);
+    double s[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const double2 v = pr[j];
+      s[j] = v.x + v.y;
+    }
+    const double rs = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+    yo[h] = rs + sc.yC[o];
   }
   __builtin_amdgcn_wave_barrier();
 }
