@@ -14,6 +14,7 @@
 //   solve_kernel     exact per-entity Cholesky (north-star "exact" mode)
 // Wave = 64 lanes throughout; no CUDA idioms.
 #include <cstdlib>
+#include <utility>
 
 #include "mr_internal.h"
 
@@ -26,15 +27,65 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 // ---------------------------------------------------------------------------
 // helpers
 // ---------------------------------------------------------------------------
+// Cross-lane sums without the LDS: v + v[lane ^ 16] and v + v[lane ^ 32] by
+// the gfx950 v_permlane16_swap / v_permlane32_swap (called with vdst = vsrc = v
+// they return {own rows, partner rows} in one order or the other, and the
+// fp add commutes, so every lane gets exactly v + v[lane ^ S]); lane ^ 8 /
+// ^ 4 / ^ 2 / ^ 1 by DPP.  Bit-identical to the __shfl_xor butterflies they
+// replace (which went through ds_bpermute), one VALU op per 32-bit half.
+template <int S>
+__device__ __forceinline__ uint32_t xor_swap_u32(uint32_t v, uint32_t& other) {
+  if constexpr (S == 16) {
+    const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    other = p[1];
+    return p[0];
+  } else {
+    const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    other = p[1];
+    return p[0];
+  }
+}
+template <int S>
+__device__ __forceinline__ double xor_sum_f64(double v) {   // S = 16 or 32
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  uint32_t lo1, hi1;
+  const uint32_t lo0 = xor_swap_u32<S>((uint32_t)u, lo1);
+  const uint32_t hi0 = xor_swap_u32<S>((uint32_t)(u >> 32), hi1);
+  return __builtin_bit_cast(double, ((uint64_t)hi0 << 32) | lo0) +
+         __builtin_bit_cast(double, ((uint64_t)hi1 << 32) | lo1);
+}
+template <int S>
+__device__ __forceinline__ float xor_sum_f32(float v) {
+  uint32_t o;
+  const uint32_t a = xor_swap_u32<S>(__builtin_bit_cast(uint32_t, v), o);
+  return __builtin_bit_cast(float, a) + __builtin_bit_cast(float, o);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v);
+
+// Butterfly over the wave (xor 32, 16, 8, 4, 2, 1): every lane gets the sum,
+// in the same bits.  Within a 16-lane row, row_ror:8 is lane ^ 8 and, once
+// the values are symmetric under ^ 8, row_ror:4 acts as lane ^ 4.
 __device__ __forceinline__ double wave_sum_f64(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v = xor_sum_f64<32>(v);
+  v = xor_sum_f64<16>(v);
+  v += dpp_f64<0x128>(v);
+  v += dpp_f64<0x124>(v);
+  v += dpp_f64<0x4E>(v);
+  return v + dpp_f64<0xB1>(v);
 }
 __device__ __forceinline__ float wave_sum_f32(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v = xor_sum_f32<32>(v);
+  v = xor_sum_f32<16>(v);
+  v += dpp_f32<0x128>(v);
+  v += dpp_f32<0x124>(v);
+  v += dpp_f32<0x4E>(v);
+  return v + dpp_f32<0xB1>(v);
 }
 
 // Fixed-order block reduction of one double per thread (deterministic).
@@ -56,7 +107,7 @@ __device__ __forceinline__ double block_sum_f64(double v, double* sh) {
 // quad_perm 0xB1 = lane ^ 1, 0x4E = lane ^ 2 (inside a quad); row_ror 0x124
 // / 0x128 rotate a 16-lane row by 4 / 8.
 template <int CTRL>
-__device__ __forceinline__ double dpp_f64(double v) {
+__device__ __forceinline__ double dpp_f64(double v) {   // declared above
   const uint64_t u = __builtin_bit_cast(uint64_t, v);
   const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
   const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
@@ -417,8 +468,8 @@ __device__ __forceinline__ void acc_matvec(const floatx4 (&acc)[NB * (NB + 1) / 
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    c += __shfl_xor(c, 16, 64);
-    c += __shfl_xor(c, 32, 64);   // identical in all 4 rows
+    c = xor_sum_f64<16>(c);
+    c = xor_sum_f64<32>(c);   // identical in all 4 rows
     if (q == 0) sc.yC[16 * bj + col] = c;
   }
   __builtin_amdgcn_wave_barrier();
@@ -588,20 +639,33 @@ typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
-// Lane (q, col) gathers rows 8q .. 8q+7 of half `half` (ids / weights
-// broadcast from lanes 32 half + 8q + t), NB contiguous floats each from its
-// column base Fc (natural columns NB col .. NB col + NB-1 = virtual (b, col)).
+// Lane (q, col) gathers rows 8q .. 8q+7 of a 32-rating half, NB contiguous
+// floats each from its column base Fc (natural columns NB col .. NB col +
+// NB-1 = virtual (b, col)).  Rating 8q + t of the half sits in lane 16q + t
+// (and 16q + 8 + t) of the ChunkRegs (half_slot), so its id / weight reach the
+// 16 lanes of row q by one DPP row_newbcast:t (no LDS permute).
+__device__ __forceinline__ int half_slot(int lane) { return 8 * (lane >> 4) + (lane & 7); }
+template <int T>
+__device__ __forceinline__ int row_bcast(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, 0x150 + T, 0xF, 0xF, false);
+}
+template <int NB, int T>
+__device__ __forceinline__ void gather_row(float (&f)[8][NB], float (&w)[8], ChunkRegs cr,
+                                           const char* __restrict__ Fc, uint32_t row_bytes) {
+  const int ri = row_bcast<T>(cr.idx);
+  w[T] = __builtin_bit_cast(float, row_bcast<T>(__builtin_bit_cast(int, cr.w)));
+  load_row_seg<NB>(f[T], reinterpret_cast<const float*>(Fc + (uint64_t)(uint32_t)ri * row_bytes));
+}
+template <int NB, int... T>
+__device__ __forceinline__ void gather_rows(float (&f)[8][NB], float (&w)[8], ChunkRegs cr,
+                                            const char* __restrict__ Fc, uint32_t row_bytes,
+                                            std::integer_sequence<int, T...>) {
+  (gather_row<NB, T>(f, w, cr, Fc, row_bytes), ...);
+}
 template <int NB>
 __device__ __forceinline__ void gather_half(float (&f)[8][NB], float (&w)[8], ChunkRegs cr,
-                                            int half, const char* __restrict__ Fc,
-                                            uint32_t row_bytes, int q) {
-#pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    const int src = 32 * half + 8 * q + t;
-    const int ri = __shfl(cr.idx, src, 64);
-    w[t] = __shfl(cr.w, src, 64);
-    load_row_seg<NB>(f[t], reinterpret_cast<const float*>(Fc + (uint64_t)(uint32_t)ri * row_bytes));
-  }
+                                            const char* __restrict__ Fc, uint32_t row_bytes) {
+  gather_rows<NB>(f, w, cr, Fc, row_bytes, std::make_integer_sequence<int, 8>{});
 }
 
 // rhs c = sum a w and (user side) row sums, fp32 on VALU, per lane over its
@@ -706,8 +770,9 @@ __device__ __forceinline__ void gram_wave(
   // one iteration and only VALU results (P) cross the back-edge, so no
   // register copy there ever waits on a load in flight.
   const int64_t safe = wlen > 0 ? wbeg : 0;    // an address every wave may read
+  const int slot = half_slot(lane);
   auto ld32 = [&](int c) {
-    const int64_t jj = wbeg + 32 * (int64_t)c + (lane & 31);
+    const int64_t jj = wbeg + 32 * (int64_t)c + slot;
     ChunkRaw r;
     const int64_t js = jj < end ? jj : safe;
     r.idx = idx[js];
@@ -717,12 +782,12 @@ __device__ __forceinline__ void gram_wave(
   };
   auto bias32 = [&](ChunkRaw& cr, int c) {
     if (!USER) {
-      const bool ok = wbeg + 32 * (int64_t)c + (lane & 31) < end;
+      const bool ok = wbeg + 32 * (int64_t)c + slot < end;
       cr.b = bias[ok ? cr.idx : zrow];
     }
   };
   auto fin32 = [&](const ChunkRaw& cr, int c) {
-    const bool ok = wbeg + 32 * (int64_t)c + (lane & 31) < end;
+    const bool ok = wbeg + 32 * (int64_t)c + slot < end;
     ChunkRegs r;
     r.idx = ok ? cr.idx : zrow;
     r.w = ok ? cr.r - cr.b : 0.f;
@@ -734,13 +799,13 @@ __device__ __forceinline__ void gram_wave(
   bias32(h1, 1);
   float Fr[8][NB], w[8];
   u32x4_t P[3][NB];
-  gather_half<NB>(Fr, w, fin32(h0, 0), 0, Fc, row_bytes, q);
+  gather_half<NB>(Fr, w, fin32(h0, 0), Fc, row_bytes);
   bf3_split<NB, USER>(P, cacc, sacc, wsum, Fr, w);
   const int nhalves = (wlen + 31) >> 5;
   for (int h = 0; h < nhalves; ++h) {
     const ChunkRaw h3 = ld32(h + 3);
     bias32(h2, h + 2);
-    gather_half<NB>(Fr, w, fin32(h1, h + 1), 0, Fc, row_bytes, q);
+    gather_half<NB>(Fr, w, fin32(h1, h + 1), Fc, row_bytes);
     bf3_mfma<NB>(acc, P);
     __builtin_amdgcn_sched_barrier(0);
     bf3_split<NB, USER>(P, cacc, sacc, wsum, Fr, w);
@@ -751,11 +816,11 @@ __device__ __forceinline__ void gram_wave(
   // ---- epilogue -----------------------------------------------------------
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    cacc[b] += __shfl_xor(cacc[b], 16, 64);
-    cacc[b] += __shfl_xor(cacc[b], 32, 64);
+    cacc[b] = xor_sum_f32<16>(cacc[b]);
+    cacc[b] = xor_sum_f32<32>(cacc[b]);
     if (USER) {
-      sacc[b] += __shfl_xor(sacc[b], 16, 64);
-      sacc[b] += __shfl_xor(sacc[b], 32, 64);
+      sacc[b] = xor_sum_f32<16>(sacc[b]);
+      sacc[b] = xor_sum_f32<32>(sacc[b]);
     }
   }
   const bool to_slab = wslab >= 0;
@@ -771,41 +836,50 @@ __device__ __forceinline__ void gram_wave(
       if (USER) D.Gs[di * D.sV + c] = (c < k) ? sacc[b] : 0.f;
     }
   }
-  const float wt = USER ? (__shfl(wsum, 0, 64) + __shfl(wsum, 16, 64)) +
-                              (__shfl(wsum, 32, 64) + __shfl(wsum, 48, 64))
+  auto lane_f32 = [](float v, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+  };
+  const float wt = USER ? (lane_f32(wsum, 0) + lane_f32(wsum, 16)) +
+                              (lane_f32(wsum, 32) + lane_f32(wsum, 48))
                         : 0.f;
   if (USER && lane == 0) {
     D.Cb[di * D.sS] = wt;
     D.Gn[di * D.sS] = (float)wlen;
   }
   // tri16 layout (mr_internal.h): off-diagonal blocks as full tiles, diagonal
-  // blocks folded pairwise; every store index is compile-time except the lane
+  // blocks folded pairwise.  Branch-free: every lane stores all 4 rows of
+  // every tile (a folded tile takes D_2m or D_2m+1 by a select), so the only
+  // masked store is the side array; store offsets are compile-time except the
+  // lane's 64 q + col.  (Per-element masked stores cost ~400 instructions of
+  // exec-mask branches per wave.)  Plain stores: 4-byte sc1 write-through
+  // stores, to keep the gathered rows in L2, made the kernel 4 % slower.
   constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2, NTILE = NO + NF + (NB & 1);
-  // (plain stores: 4-byte sc1 write-through stores, to keep the gathered rows
-  // in L2, made the kernel 4 % slower -- users 884 -> 924 us)
-  auto st = [&](int64_t off, float v) { Gd[off] = v; };
-  int t = 0;
+  float* __restrict__ Gl = Gd + 64 * q + col;
 #pragma unroll
   for (int bi = 0; bi < NB; ++bi) {
 #pragma unroll
-    for (int bj = bi; bj < NB; ++bj) {
+    for (int bj = bi + 1; bj < NB; ++bj) {
+      const int t = acc_tile(bi, bj, NB), o = off_index(bi, bj, NB) * 256;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 4 * q + r;
-        const float v = acc[t][r];
-        if (bi != bj) {
-          st(off_index(bi, bj, NB) * 256 + row * 16 + col, v);
-        } else if ((NB & 1) && bi == NB - 1) {
-          st((NO + NF) * 256 + row * 16 + col, v);
-        } else if ((bi & 1) == 0) {
-          if (col >= row) st((NO + (bi >> 1)) * 256 + row * 16 + col, v);
-        } else {
-          if (col < row) st((NO + (bi >> 1)) * 256 + row * 16 + col, v);
-          else if (col == row) st(NTILE * 256 + (bi >> 1) * 16 + row, v);
-        }
-      }
-      ++t;
+      for (int r = 0; r < 4; ++r) Gl[o + 16 * r] = acc[t][r];
     }
+  }
+#pragma unroll
+  for (int m = 0; m < NF; ++m) {
+    const int te = acc_tile(2 * m, 2 * m, NB), to = acc_tile(2 * m + 1, 2 * m + 1, NB);
+    float dg = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 4 * q + r;
+      Gl[(NO + m) * 256 + 16 * r] = col >= row ? acc[te][r] : acc[to][r];
+      if (col - 4 * q == r) dg = acc[to][r];
+    }
+    if ((col >> 2) == q) Gd[NTILE * 256 + m * 16 + col] = dg;   // D_2m+1's diagonal
+  }
+  if constexpr ((NB & 1) != 0) {
+    const int t = acc_tile(NB - 1, NB - 1, NB);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Gl[(NO + NF) * 256 + 16 * r] = acc[t][r];
   }
   if constexpr (FUSE) {
     if (!to_slab)
