@@ -63,7 +63,7 @@ __device__ __forceinline__ float xor_sum_f32(float v) {
 template <int CTRL>
 __device__ __forceinline__ float dpp_f32(float v) {
   return __builtin_bit_cast(
-      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+      float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
 }
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v);
@@ -109,8 +109,8 @@ __device__ __forceinline__ double block_sum_f64(double v, double* sh) {
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {   // declared above
   const uint64_t u = __builtin_bit_cast(uint64_t, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
   return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo);
 }
 // Sum over the 4 lanes of a quad; every lane of the quad gets the same value.
@@ -647,7 +647,7 @@ typedef float f32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ int half_slot(int lane) { return 8 * (lane >> 4) + (lane & 7); }
 template <int T>
 __device__ __forceinline__ int row_bcast(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, 0x150 + T, 0xF, 0xF, false);
+  return __builtin_amdgcn_mov_dpp(v, 0x150 + T, 0xF, 0xF, false);
 }
 template <int NB, int T>
 __device__ __forceinline__ void gather_row(float (&f)[8][NB], float (&w)[8], ChunkRegs cr,
@@ -684,19 +684,43 @@ __device__ __forceinline__ void bf3_split(u32x4_t (&P)[3][NB], float (&cacc)[NB]
     }
     if (USER) wsum += w[t];
   }
+  // a = h + m + l per float: r = a - h, l = r - m (h, m = the value with its
+  // low 16 bits cleared).  Two floats per packed subtract, taken along the
+  // row -- (t, b) and (t, b+1) sit in adjacent registers of the row's gather
+  // -- so no register moves are needed; the bf16 pairs of ratings (2j, 2j+1)
+  // are then packed by v_perm.
 #pragma unroll
-  for (int b = 0; b < NB; ++b) {
+  for (int j = 0; j < 4; ++j) {
+    uint32_t R[2][NB], L[2][NB];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const f32x2_t x = {f[2 * j][b], f[2 * j + 1][b]};
-      const u32x2_t xa = __builtin_bit_cast(u32x2_t, x);
-      const f32x2_t r = x - __builtin_bit_cast(f32x2_t, xa & 0xFFFF0000u);   // v_pk_add_f32
-      const u32x2_t ra = __builtin_bit_cast(u32x2_t, r);
-      const f32x2_t sv = r - __builtin_bit_cast(f32x2_t, ra & 0xFFFF0000u);
-      const u32x2_t sa = __builtin_bit_cast(u32x2_t, sv);
-      P[0][b][j] = __builtin_amdgcn_perm(xa[1], xa[0], 0x07060302u);
-      P[1][b][j] = __builtin_amdgcn_perm(ra[1], ra[0], 0x07060302u);
-      P[2][b][j] = __builtin_amdgcn_perm(sa[1], sa[0], 0x07060302u);
+    for (int u = 0; u < 2; ++u) {
+      const float (&a)[NB] = f[2 * j + u];
+#pragma unroll
+      for (int b = 0; b + 1 < NB; b += 2) {
+        const f32x2_t x = {a[b], a[b + 1]};
+        const u32x2_t xa = __builtin_bit_cast(u32x2_t, x);
+        const f32x2_t r = x - __builtin_bit_cast(f32x2_t, xa & 0xFFFF0000u);   // v_pk_add_f32
+        const u32x2_t ra = __builtin_bit_cast(u32x2_t, r);
+        const u32x2_t la =
+            __builtin_bit_cast(u32x2_t, r - __builtin_bit_cast(f32x2_t, ra & 0xFFFF0000u));
+        R[u][b] = ra[0]; R[u][b + 1] = ra[1];
+        L[u][b] = la[0]; L[u][b + 1] = la[1];
+      }
+      if constexpr ((NB & 1) != 0) {
+        const uint32_t xa = __builtin_bit_cast(uint32_t, a[NB - 1]);
+        const float r = a[NB - 1] - __builtin_bit_cast(float, xa & 0xFFFF0000u);
+        const uint32_t ra = __builtin_bit_cast(uint32_t, r);
+        R[u][NB - 1] = ra;
+        L[u][NB - 1] =
+            __builtin_bit_cast(uint32_t, r - __builtin_bit_cast(float, ra & 0xFFFF0000u));
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      P[0][b][j] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, f[2 * j + 1][b]),
+                                         __builtin_bit_cast(uint32_t, f[2 * j][b]), 0x07060302u);
+      P[1][b][j] = __builtin_amdgcn_perm(R[1][b], R[0][b], 0x07060302u);
+      P[2][b][j] = __builtin_amdgcn_perm(L[1][b], L[0][b], 0x07060302u);
     }
   }
 }
@@ -739,7 +763,7 @@ __device__ __forceinline__ void gram_wave(
   const int wslab = work[wi].slab;
   const int q = lane >> 4, col = lane & 15;
   const int64_t end = wbeg + wlen;
-  const uint32_t row_bytes = (uint32_t)ldk * 4u;
+  constexpr uint32_t row_bytes = 64u * NB;     // ldk = 16 NB floats
   const char* Fc = reinterpret_cast<const char*>(F) + 4 * NB * col;
 
   // fused CG start: this lane's x entries (virtual (b, col) = natural
