@@ -162,6 +162,8 @@ def main():
                     help="start CG with a matvec + update pass instead of the Gram epilogue")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="time steps without per-launch HIP events (no roofline)")
+    ap.add_argument("--cg-speculate", type=int, default=None,
+                    help="engine launch-ahead level (include/mr_als.h MR_OPT_CG_SPECULATE)")
     ap.add_argument("--cpu-scale", type=float, default=0.25)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--force-shard", action="store_true",
@@ -234,6 +236,8 @@ def main():
         ctx.set_factors(U0, V0)
     if args.no_fuse_start:
         ctx.set_option("fuse_start", 0)
+    if args.cg_speculate is not None:
+        ctx.set_option("cg_speculate", args.cg_speculate)
     ctx.sync()
     log(f"[bench] context built in {time.perf_counter() - t0:.2f} s")
 

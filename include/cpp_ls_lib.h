@@ -11,8 +11,9 @@
  * Differences (documented in INTEGRATION.md):
  *   - failures return a negative value and log to stderr (the reference throws
  *     across extern "C" -> std::terminate, matrix.cpp:403-405, 422-424);
- *   - arithmetic runs on the GPU: ALS in fp32 (normal equations, CG vectors)
- *     with fp64 CG scalars; the general CG least squares in fp64;
+ *   - arithmetic runs on the GPU: ALS normal equations and factors in fp32,
+ *     CG vectors, products and scalars in fp64; the general CG least squares
+ *     in fp64;
  *   - no caller pointer is retained after return.
  */
 #ifndef MR_CPP_LS_LIB_H

@@ -130,7 +130,9 @@ int mr_als_set_timing(mr_als* ctx, int enable);
  *   MR_OPT_CG_SPECULATE   1 (default): enqueue CG iteration t+1 before t's
  *                         state is read back when t provably cannot stop
  *                         (decided on exact per-iteration states: identical
- *                         launches on every rank); 0: one iteration ahead
+ *                         launches on every rank); 0: one iteration ahead;
+ *                         2: always two ahead (an iteration launched after
+ *                         the solve stopped exits at once: results identical)
  *   MR_OPT_WAIT_TIMEOUT_S host wait for a published CG state, seconds
  *                         (default 300; a stalled peer rank then fails the
  *                         call instead of hanging it) */
@@ -186,7 +188,7 @@ void* mr_als_stream(mr_als* ctx);
 long long mr_als_num_ratings(mr_als* ctx);
 
 /* Device-side pointers of the fp32 factor tables (row stride ldk floats,
- * ldk = k rounded up to 4): Ufac[U*ldk], Ubias[U], Vfac[I*ldk]. */
+ * ldk = k rounded up to 16): Ufac[U*ldk], Ubias[U], Vfac[I*ldk]. */
 int mr_als_device_tables(mr_als* ctx, float** Ufac, float** Ubias,
                          float** Vfac, int* ldk);
 

@@ -76,9 +76,9 @@ int mr_rec_top_n(mr_rec* ctx, int n_users, const double* x, const long long* exc
  * agreement[t] = compute_ranking_agreement of the scorable ratings, NaN when
  * the reference returns None; n_agree / n_disagree = its pair counts.
  * pred (optional): the prediction of every test rating (NaN for -1).
- * sse (optional): sum over scorable ratings of (pred - actual)^2, n_pred
- * (optional): their number -- the held-out RMSE the reference does not
- * report. */
+ * sse / n_pred (optional): [n_test] -- per test user, the sum over its
+ * scorable ratings of (pred - actual)^2 and their number (the held-out RMSE
+ * the reference does not report is sqrt(sum sse / sum n_pred)). */
 int mr_rec_evaluate(mr_rec* ctx, int n_rows, const double* U, int n_test,
                     const int* user_row, const long long* off, const int* cand,
                     const double* actual, double* agreement, long long* n_agree,

@@ -239,7 +239,7 @@ int mr_als_set_option(mr_als* ctx, int option, double value) {
   MR_CHECK(ctx, "null context");
   switch (option) {
     case MR_OPT_FUSE_START: ctx->eng.fuse_start = value != 0.0; return 0;
-    case MR_OPT_CG_SPECULATE: ctx->eng.speculate = value != 0.0; return 0;
+    case MR_OPT_CG_SPECULATE: ctx->eng.speculate = (int)value; return 0;
     case MR_OPT_WAIT_TIMEOUT_S:
       MR_CHECK(value > 0.0, "timeout must be > 0");
       ctx->eng.wait_timeout_s = value;

@@ -78,7 +78,8 @@ struct Engine {
   double ridge = 0.0;
   int chunk = 2048;
   bool fuse_start = true;   // CG start in the Gram epilogue (MR_OPT_FUSE_START)
-  bool speculate = true;    // enqueue CG iteration t+1 before t's state is known
+  int speculate = 1;        // 0: never enqueue ahead; 1: enqueue t+2 while t+1 runs when
+                            // state t proves t+1 cannot stop; 2: always one ahead
                             // when t provably cannot stop (MR_OPT_CG_SPECULATE;
                             // decided on exact published states, so every rank
                             // of a sharded run issues the same launches)

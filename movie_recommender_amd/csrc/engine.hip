@@ -715,7 +715,7 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr, bool start
   //     (fails == 0, rr far above 1e-6, t+2 < max_it) -- the stream stays
   //     busy while the host waits for the state after t+1;
   //   * iteration t+1 publishes (S not done => it is not a no-op).
-  const int spec = speculate ? 1 : 0;
+  const int spec = speculate;
   int launched = 0;          // iterations enqueued so far
   for (; launched < std::min(spec ? 2 : 1, max_it); ++launched)
     if (launch_iter(launched)) return -1;
@@ -727,7 +727,8 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr, bool start
       if (launch_iter(launched)) return -1;
       ++launched;
     }
-    if (spec && launched == known + 2 && ms.fails == 0 && ms.rr > 1e-4 && known + 2 < max_it) {
+    if (spec && launched == known + 2 && known + 2 < max_it &&
+        (spec >= 2 || (ms.fails == 0 && ms.rr > 1e-4))) {
       if (launch_iter(launched)) return -1;
       ++launched;
     }
@@ -762,7 +763,8 @@ int Engine::half_step(bool user, double min_dec, int max_it, double* final_rr) {
   MR_HIP(hipSetDevice(device));
   Side& S = user ? su : si;
   const size_t g0 = pending.size();
-  const bool fused = solver == MR_SOLVER_CG && fuse_start;
+  // the CG start rides on the MFMA Gram's accumulators (k >= 32 only)
+  const bool fused = solver == MR_SOLVER_CG && fuse_start && k >= kMfmaMinK;
   if (gram(S, fused)) return -1;
   const size_t c0 = pending.size();
   int its = 0;

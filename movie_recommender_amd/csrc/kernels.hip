@@ -973,10 +973,143 @@ static int launch_gram_nb(hipStream_t s, bool user_side, int k, const WorkItem* 
   return 0;
 }
 
+// ---------------------------------------------------------------------------
+// K1 for k < 32 (NB <= 2): the same normal equations on the VALU, fp32 FMAs
+// in rating order (north star: matrix cores only for k >= 32; a 16 x 16 MFMA
+// tile would waste most of its work on k = 10).  One wave per work item;
+// chunks of 64 ratings: lane t gathers rating t's factor row into LDS in
+// virtual order (v = 16 b + i <-> n = NB i + b, mr_internal.h), then every
+// lane accumulates its entries over the chunk.  Lane l owns virtual rows
+// rr + 16 bi (rr = l >> 2) and columns c4 + 16 bj .. + 3 (c4 = 4 (l & 3)) of
+// the upper blocks (bi <= bj), diagonal blocks in full, so its 4 entries of a
+// block are exactly float4 l of that block's row-major tile: the tri16 stores
+// are one float4 per lane per tile.  rhs c (and, user side, the row sums) in
+// the lanes' rows; the count / rating sum are wave-uniform.
+// ---------------------------------------------------------------------------
+template <int NB, bool USER>
+__global__ __launch_bounds__(256) void gram_valu_kernel(
+    const WorkItem* __restrict__ work, int64_t n_work, const int32_t* __restrict__ idx,
+    const float* __restrict__ val, const float* __restrict__ F, const float* __restrict__ bias,
+    int k, int zrow, GramDst direct, GramDst slab) {
+  static_assert(NB == 1 || NB == 2, "VALU Gram: k < 32");
+  constexpr int LD = 16 * NB;                 // ldk, floats per factor row
+  constexpr int NBLK = NB * (NB + 1) / 2;     // upper blocks
+  __shared__ float rows[4][64][LD + 1];       // +1: rows of a chunk on distinct banks
+  __shared__ float wts[4][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t wi = (int64_t)blockIdx.x * 4 + wid;
+  if (wi >= n_work) return;
+  const int64_t wbeg = work[wi].begin;
+  const int wlen = work[wi].len;
+  const int went = work[wi].entity, wslab = work[wi].slab;
+  const int rr = lane >> 2, c4 = 4 * (lane & 3);
+  float acc[NBLK][4];
+#pragma unroll
+  for (int t = 0; t < NBLK; ++t) acc[t][0] = acc[t][1] = acc[t][2] = acc[t][3] = 0.f;
+  float cacc[NB], sacc[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) cacc[b] = sacc[b] = 0.f;
+  float wsum = 0.f;
+  float (&R)[64][LD + 1] = rows[wid];
+  for (int base = 0; base < wlen; base += 64) {
+    const int n = min(64, wlen - base);
+    {
+      const bool ok = lane < n;
+      const int id = ok ? idx[wbeg + base + lane] : zrow;
+      float w = ok ? val[wbeg + base + lane] : 0.f;
+      if (!USER) w -= bias[id];              // r - U[u][k] (fill_ratings_minus_bias); 0 - 0 past the end
+      const float4* src = reinterpret_cast<const float4*>(F + (int64_t)id * LD);
+#pragma unroll
+      for (int h = 0; h < LD / 4; ++h) {
+        const float4 a = src[h];
+        const float e[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          const int nn = 4 * h + x;            // natural column
+          R[lane][16 * (nn % NB) + nn / NB] = e[x];
+        }
+      }
+      wts[wid][lane] = w;
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int t = 0; t < n; ++t) {
+      const float w = wts[wid][t];
+      float ar[NB], ac[NB][4];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        ar[b] = R[t][16 * b + rr];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) ac[b][x] = R[t][16 * b + c4 + x];
+      }
+      int blk = 0;
+#pragma unroll
+      for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+        for (int bj = bi; bj < NB; ++bj, ++blk)
+#pragma unroll
+          for (int x = 0; x < 4; ++x) acc[blk][x] = fmaf(ar[bi], ac[bj][x], acc[blk][x]);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        cacc[b] = fmaf(ar[b], w, cacc[b]);
+        if (USER) sacc[b] += ar[b];
+      }
+      if (USER) wsum += w;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  // epilogue: tri16 tiles (NB = 1: one full tile; NB = 2: tile 0 = block
+  // (0,1), tile 1 = D0 upper with D1's strict lower, side array = D1's diagonal)
+  const bool to_slab = wslab >= 0;
+  const int64_t di = to_slab ? (int64_t)wslab : (int64_t)went;
+  const GramDst& D = to_slab ? slab : direct;
+  float4* Gt = reinterpret_cast<float4*>(D.G + di * D.sG);
+  if constexpr (NB == 1) {
+    Gt[lane] = make_float4(acc[0][0], acc[0][1], acc[0][2], acc[0][3]);
+  } else {
+    Gt[lane] = make_float4(acc[1][0], acc[1][1], acc[1][2], acc[1][3]);   // block (0,1)
+    float f[4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) f[x] = (c4 + x >= rr) ? acc[0][x] : acc[2][x];
+    Gt[64 + lane] = make_float4(f[0], f[1], f[2], f[3]);
+    if ((rr >> 2) == (lane & 3)) {   // this lane holds D1[rr][rr]
+      const int x = rr - c4;
+      const float dv = x == 0 ? acc[2][0] : x == 1 ? acc[2][1] : x == 2 ? acc[2][2] : acc[2][3];
+      D.G[di * D.sG + 512 + rr] = dv;
+    }
+  }
+  if ((lane & 3) == 0) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int nn = NB * rr + b;   // natural column of virtual (b, rr)
+      D.C[di * D.sV + nn] = nn < k ? cacc[b] : 0.f;
+      if (USER) D.Gs[di * D.sV + nn] = nn < k ? sacc[b] : 0.f;
+    }
+  }
+  if (USER && lane == 0) {
+    D.Cb[di * D.sS] = wsum;
+    D.Gn[di * D.sS] = (float)wlen;
+  }
+}
+
 int launch_gram(hipStream_t s, bool user_side, int k, const WorkItem* work,
                 int64_t n_work, const int32_t* idx, const float* val,
                 const float* F, const float* bias, int zrow, GramDst direct,
                 GramDst slab, const CgStart* start) {
+  if (k < kMfmaMinK) {
+    MR_CHECK(start == nullptr, "k < 32: the VALU Gram has no fused CG start");
+    if (n_work <= 0) return 0;
+    const dim3 grid((unsigned)((n_work + 3) / 4));
+#define MR_VG(NB, U) \
+  MR_LAUNCH((gram_valu_kernel<NB, U>), grid, dim3(256), 0, s, work, n_work, idx, val, F, bias, k, zrow, direct, slab)
+    if (k <= 16) {
+      if (user_side) MR_VG(1, true); else MR_VG(1, false);
+    } else {
+      if (user_side) MR_VG(2, true); else MR_VG(2, false);
+    }
+#undef MR_VG
+    MR_HIP(hipGetLastError());
+    return 0;
+  }
 #define MR_GRAM_CASE(NB) \
   case NB: return launch_gram_nb<NB>(s, user_side, k, work, n_work, idx, val, F, bias, zrow, direct, slab, start);
   switch (nb16_of(k)) {

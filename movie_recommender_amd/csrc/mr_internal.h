@@ -77,6 +77,7 @@ extern thread_local Stager t_stager;
   } while (0)
 
 constexpr int kMaxK = 128;        // largest factor count the Gram kernel tiles
+constexpr int kMfmaMinK = 32;     // k < 32: VALU Gram (gram_valu_kernel), no fused CG start
 // Row stride of factor tables / CG vectors: k rounded up to a multiple of 16
 // (one 16-wide block of the tri16 storage), so every Gram lane's NB-float segment of a row
 // lies inside the row; padding columns are kept at zero.
