@@ -80,7 +80,8 @@ typedef struct mr_comm {
 } mr_comm;
 
 /* Context from host COO ratings (zero-based ids).  Builds the by-user and
- * by-item CSR on the device.  k <= 128.  NULL on error (see mr_last_error). */
+ * by-item CSR on the device.  k <= 512 (k > 128 runs the streamed large-k
+ * kernels; the exact solver needs k <= 128).  NULL on error (mr_last_error). */
 mr_als* mr_als_create(int device, int k, int num_users, int num_items,
                       long long n_ratings, const int* user_ids,
                       const int* item_ids, const double* ratings);

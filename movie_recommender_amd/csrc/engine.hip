@@ -253,7 +253,7 @@ int Engine::init(int dev, int k_, int64_t U_, int64_t I_, int64_t n_u,
   ldk = ldk_of(k);
   U = U_;
   I = I_;
-  MR_CHECK(k >= 1 && k <= kMaxK, "k must be in [1, 128]");
+  MR_CHECK(k >= 1 && k <= kMaxKLarge, "k must be in [1, 512]");
   MR_CHECK(U >= 0 && I >= 0, "negative table size");
   MR_CHECK(0 <= u0 && u0 <= u1 && u1 <= U && 0 <= i0 && i0 <= i1 && i1 <= I,
            "bad shard range");
@@ -763,8 +763,8 @@ int Engine::half_step(bool user, double min_dec, int max_it, double* final_rr) {
   MR_HIP(hipSetDevice(device));
   Side& S = user ? su : si;
   const size_t g0 = pending.size();
-  // the CG start rides on the MFMA Gram's accumulators (k >= 32 only)
-  const bool fused = solver == MR_SOLVER_CG && fuse_start && k >= kMfmaMinK;
+  // the CG start rides on the MFMA Gram's accumulators (32 <= k <= 128)
+  const bool fused = solver == MR_SOLVER_CG && fuse_start && k >= kMfmaMinK && k <= kMaxK;
   if (gram(S, fused)) return -1;
   const size_t c0 = pending.size();
   int its = 0;

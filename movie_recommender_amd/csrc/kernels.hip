@@ -1091,10 +1091,170 @@ __global__ __launch_bounds__(256) void gram_valu_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// K1 for k > 128 (NB > 8): the reference has no limit on k, but a wave's
+// registers cannot hold NB(NB+1)/2 accumulator tiles past NB = 8.  This form
+// trades speed for generality: block (work item, group of 16 stored tri16
+// tiles); 32-rating chunks of rows are staged in LDS in virtual order and
+// every thread accumulates 4 entries (a row segment of 4 columns, one float4
+// of the row-major tile) of each of its group's tiles in fp32, rating order.
+// The gathers repeat once per tile group (ceil(NTILE / 16) groups).  Group 0
+// also forms the rhs, row sums, rating sum and count.
+// ---------------------------------------------------------------------------
+constexpr int LK_ROWS = 32;     // ratings per staged chunk
+constexpr int LK_TILES = 16;    // stored tiles per block: 4 tiles x 64 threads, 4 passes
+
+template <bool USER>
+__global__ __launch_bounds__(256) void gram_largek_kernel(
+    const WorkItem* __restrict__ work, const int32_t* __restrict__ idx,
+    const float* __restrict__ val, const float* __restrict__ F, const float* __restrict__ bias,
+    int k, int zrow, GramDst direct, GramDst slab) {
+  extern __shared__ float lk_sm[];
+  const int NB = nb16_of(k), ldk = 16 * NB;
+  const int NO = n_off_of(NB), NF = n_fold_of(NB), NTILE = n_tiles_of(NB);
+  float* rows = lk_sm;                           // [LK_ROWS][ldk + 1], virtual order
+  float* wts = lk_sm + LK_ROWS * (ldk + 1);      // [LK_ROWS]
+  const int ld = ldk + 1;
+  const int64_t wi = blockIdx.x;
+  const int64_t wbeg = work[wi].begin;
+  const int wlen = work[wi].len, went = work[wi].entity, wslab = work[wi].slab;
+  const int tid = threadIdx.x, lane = tid & 63, sub = tid >> 6;
+  const int rr = lane >> 2, c4 = 4 * (lane & 3);
+  const int group = blockIdx.y;
+  // this thread's tiles: group * 16 + 4 j + sub; kind 0 = off-diagonal (bi, bj),
+  // 1 = fold m (D_2m upper incl. diagonal, D_2m+1 strict lower), 2 = odd last
+  int kind[4], ra[4], rb[4], ca[4], cb[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int t = group * LK_TILES + 4 * j + sub;
+    kind[j] = -1; ra[j] = rb[j] = ca[j] = cb[j] = 0;
+    if (t < NO) {
+      int bi = 0, rem = t;
+      while (rem >= NB - 1 - bi) { rem -= NB - 1 - bi; ++bi; }
+      const int bj = bi + 1 + rem;
+      kind[j] = 0; ra[j] = 16 * bi + rr; ca[j] = 16 * bj + c4;
+    } else if (t < NO + NF) {
+      const int m = t - NO;
+      kind[j] = 1; ra[j] = 32 * m + rr; ca[j] = 32 * m + c4;
+      rb[j] = 32 * m + 16 + rr; cb[j] = 32 * m + 16 + c4;
+    } else if (t < NTILE) {
+      kind[j] = 2; ra[j] = 16 * (NB - 1) + rr; ca[j] = 16 * (NB - 1) + c4;
+    }
+  }
+  // fp64 accumulation, one rounding to fp32 at the store (this path has the
+  // registers for it; the dense k = 144 golden is ill-conditioned enough that
+  // 170-term fp32 sums land at ~8e-5 of the reference)
+  double acc[4][4], sd[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    sd[j] = 0.0;
+#pragma unroll
+    for (int x = 0; x < 4; ++x) acc[j][x] = 0.0;
+  }
+  // group 0, thread v < ldk: rhs / row sum of virtual column v
+  double cv = 0.0, sv = 0.0, wsum = 0.0;
+  for (int base = 0; base < wlen; base += LK_ROWS) {
+    const int n = min(LK_ROWS, wlen - base);
+    __syncthreads();
+    // stage: row t, float4 h; natural column nn -> virtual 16 (nn % NB) + nn / NB
+    const int q4 = ldk / 4;
+    for (int e = tid; e < LK_ROWS * q4; e += 256) {
+      const int t = e / q4, h = e - t * q4;
+      const int id = t < n ? idx[wbeg + base + t] : zrow;
+      const float4 a = reinterpret_cast<const float4*>(F + (int64_t)id * ldk)[h];
+      const float v4[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const int nn = 4 * h + x;
+        rows[t * ld + 16 * (nn % NB) + nn / NB] = v4[x];
+      }
+    }
+    if (tid < LK_ROWS) {
+      const bool ok = tid < n;
+      const int id = ok ? idx[wbeg + base + tid] : zrow;
+      float w = ok ? val[wbeg + base + tid] : 0.f;
+      if (!USER) w -= bias[id];
+      wts[tid] = w;
+    }
+    __syncthreads();
+    for (int t = 0; t < n; ++t) {
+      const float* a = rows + t * ld;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (kind[j] < 0) continue;
+        const double av = a[ra[j]];
+        if (kind[j] == 1) {
+          const double bv = a[rb[j]];
+#pragma unroll
+          for (int x = 0; x < 4; ++x) {
+            const bool up = c4 + x >= rr;          // D_2m's stored upper triangle
+            acc[j][x] = fma(up ? av : bv, (double)(up ? a[ca[j] + x] : a[cb[j] + x]), acc[j][x]);
+          }
+          sd[j] = fma(bv, bv, sd[j]);              // D_2m+1's diagonal (side array)
+        } else {
+#pragma unroll
+          for (int x = 0; x < 4; ++x) acc[j][x] = fma(av, (double)a[ca[j] + x], acc[j][x]);
+        }
+      }
+      if (group == 0 && tid < ldk) {
+        const double av = a[tid];
+        cv = fma(av, (double)wts[t], cv);
+        if (USER) sv += av;
+      }
+      if (USER) wsum += wts[t];
+    }
+  }
+  const bool to_slab = wslab >= 0;
+  const int64_t di = to_slab ? (int64_t)wslab : (int64_t)went;
+  const GramDst& D = to_slab ? slab : direct;
+  float* Ge = D.G + di * D.sG;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (kind[j] < 0) continue;
+    const int t = group * LK_TILES + 4 * j + sub;
+    reinterpret_cast<float4*>(Ge + (int64_t)t * 256)[lane] =
+        make_float4((float)acc[j][0], (float)acc[j][1], (float)acc[j][2], (float)acc[j][3]);
+    if (kind[j] == 1 && (rr >> 2) == (lane & 3))   // the thread at (rr, rr)
+      Ge[(int64_t)NTILE * 256 + (t - NO) * 16 + rr] = (float)sd[j];
+  }
+  if (group == 0) {
+    if (tid < ldk) {
+      const int nn = NB * (tid & 15) + (tid >> 4);   // natural column of virtual tid
+      D.C[di * D.sV + nn] = nn < k ? (float)cv : 0.f;
+      if (USER) D.Gs[di * D.sV + nn] = nn < k ? (float)sv : 0.f;
+    }
+    if (USER && tid == 0) {
+      D.Cb[di * D.sS] = (float)wsum;
+      D.Gn[di * D.sS] = (float)wlen;
+    }
+  }
+}
+
 int launch_gram(hipStream_t s, bool user_side, int k, const WorkItem* work,
                 int64_t n_work, const int32_t* idx, const float* val,
                 const float* F, const float* bias, int zrow, GramDst direct,
                 GramDst slab, const CgStart* start) {
+  if (k > kMaxK) {
+    MR_CHECK(start == nullptr, "k > 128: no fused CG start");
+    MR_CHECK(k <= kMaxKLarge, "k > 512 not supported");
+    if (n_work <= 0) return 0;
+    const int nb = nb16_of(k), ldk = 16 * nb;
+    const size_t lds = (size_t)(LK_ROWS * (ldk + 1) + LK_ROWS) * sizeof(float);
+    const dim3 grid((unsigned)n_work, (unsigned)((n_tiles_of(nb) + LK_TILES - 1) / LK_TILES));
+    if (user_side) {
+      MR_HIP(hipFuncSetAttribute((const void*)gram_largek_kernel<true>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      MR_LAUNCH(gram_largek_kernel<true>, grid, dim3(256), lds, s, work, idx, val, F, bias, k,
+                zrow, direct, slab);
+    } else {
+      MR_HIP(hipFuncSetAttribute((const void*)gram_largek_kernel<false>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      MR_LAUNCH(gram_largek_kernel<false>, grid, dim3(256), lds, s, work, idx, val, F, bias, k,
+                zrow, direct, slab);
+    }
+    MR_HIP(hipGetLastError());
+    return 0;
+  }
   if (k < kMfmaMinK) {
     MR_CHECK(start == nullptr, "k < 32: the VALU Gram has no fused CG start");
     if (n_work <= 0) return 0;
@@ -1466,12 +1626,164 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 4 : 1)) void cg_matvec_kernel(
   if (fst && phase == CG_ALPHA) last_block_finalize(fst, CG_ALPHA, partials, nullptr, 0, sh);
 }
 
+// K2 for k > 128: the same block GEMV (fused p update, fp64 products, p.q
+// partial, control in the last block) with the tiles streamed from memory
+// instead of held in registers: one wave per entity, two passes over the
+// entity's tri16 tiles -- block rows (4-lane quad sums into yR), then block
+// columns (16-lane column partials summed in a fixed order into yC) -- so G
+// is read twice.  Per-wave LDS: p, yR, yC (16 NB doubles each) + 256 doubles.
+template <bool USER>
+__global__ __launch_bounds__(256) void cg_matvec_largek_kernel(
+    const CgState* __restrict__ st, int update_p, int64_t E, int k,
+    const float* __restrict__ G, const float* __restrict__ Gs, const float* __restrict__ Gn,
+    double* __restrict__ v, double* __restrict__ vb, const double* __restrict__ r,
+    const double* __restrict__ rb, double* __restrict__ y, double* __restrict__ yb,
+    double* __restrict__ partials, CgState* fst, int phase) {
+  if (ald(&st->done)) return;
+  extern __shared__ double lm_sm[];
+  __shared__ double sh[MV_WAVES];
+  const int NB = nb16_of(k), ldk = 16 * NB, NP = ldk;
+  const int NO = n_off_of(NB), NF = n_fold_of(NB), NTILE = n_tiles_of(NB);
+  const int64_t GS = gsize_of(k);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  double* pv = lm_sm + (int64_t)wid * (3 * NP + 256);
+  double* yR = pv + NP;
+  double* yC = yR + NP;
+  double* red = yC + NP;
+  const int rr = lane >> 2, c4 = (lane & 3) * 4;
+  const double beta = ald(&st->beta);
+  double dsum = 0.0;
+  auto diag_tile = [&](int b, bool& lower) {
+    lower = (b & 1) && b < 2 * NF;
+    return (b < 2 * NF) ? NO + (b >> 1) : NO + NF;
+  };
+  for (int64_t e = (int64_t)blockIdx.x * MV_WAVES + wid; e < E;
+       e += (int64_t)gridDim.x * MV_WAVES) {
+    const float4* Ge = reinterpret_cast<const float4*>(G + e * GS);
+    double* ve = v + e * ldk;
+    // p = -r + beta p (matrix.cpp:521), staged in virtual order
+    for (int i = lane; i < NP; i += 64) {
+      double x = ve[i];
+      if (update_p) {
+        x = fma(beta, x, -r[e * ldk + i]);
+        ve[i] = x;
+      }
+      pv[virt_of(i, NB)] = x;
+    }
+    double vbias = USER ? vb[e] : 0.0;
+    if (USER && update_p) {
+      vbias = fma(beta, vbias, -rb[e]);
+      if (lane == 0) vb[e] = vbias;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // pass 1: block rows
+    for (int bi = 0; bi < NB; ++bi) {
+      double s0 = 0.0;
+      for (int bj = bi + 1; bj < NB; ++bj) {
+        const float4 g = Ge[(int64_t)off_index(bi, bj, NB) * 64 + lane];
+        const double ge[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+        for (int x = 0; x < 4; ++x) s0 = fma(ge[x], pv[16 * bj + c4 + x], s0);
+      }
+      bool lower;
+      const float4 g = Ge[(int64_t)diag_tile(bi, lower) * 64 + lane];
+      const double ge[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const int c = c4 + x;
+        const bool use = lower ? (c < rr) : (c >= rr);
+        s0 = fma(use ? ge[x] : 0.0, pv[16 * bi + c], s0);
+      }
+      const double rs = quad_sum_f64(s0);
+      if ((lane & 3) == 0) yR[16 * bi + rr] = rs;
+    }
+    // pass 2: block columns
+    for (int bj = 0; bj < NB; ++bj) {
+      double cc[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int bi = 0; bi < bj; ++bi) {
+        const float4 g = Ge[(int64_t)off_index(bi, bj, NB) * 64 + lane];
+        const double ge[4] = {g.x, g.y, g.z, g.w};
+        const double pi = pv[16 * bi + rr];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) cc[x] = fma(ge[x], pi, cc[x]);
+      }
+      bool lower;
+      const float4 g = Ge[(int64_t)diag_tile(bj, lower) * 64 + lane];
+      const double ge[4] = {g.x, g.y, g.z, g.w};
+      const double pr = pv[16 * bj + rr];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const int c = c4 + x;
+        const bool use = lower ? (c < rr) : (c > rr);
+        cc[x] = fma(use ? ge[x] : 0.0, pr, cc[x]);
+      }
+#pragma unroll
+      for (int x = 0; x < 4; ++x) red[4 * lane + x] = cc[x];
+      __builtin_amdgcn_wave_barrier();
+      if (lane < 16) {   // column c = lane: partials of rows rr = 0..15, fixed order
+        double sacc = 0.0;
+        for (int q = 0; q < 16; ++q) sacc += red[16 * q + lane];
+        yC[16 * bj + lane] = sacc;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    // y = row + column parts (+ side diagonals of odd folded blocks, + bias column)
+    const float* Gse = USER ? Gs + e * ldk : nullptr;
+    double d = 0.0, ybp = 0.0;
+    for (int o = lane; o < NP; o += 64) {
+      const int n = nat_of(o, NB);
+      if (n >= k) continue;
+      const int b = o >> 4, ii = o & 15;
+      double yv = yR[o] + yC[o];
+      if ((b & 1) && b < 2 * NF)
+        yv = fma((double)G[e * GS + (int64_t)NTILE * 256 + (b >> 1) * 16 + ii], pv[o], yv);
+      if (USER) {
+        const double gs = Gse[n];
+        yv = fma(gs, vbias, yv);
+        ybp = fma(gs, pv[o], ybp);
+      }
+      y[e * ldk + n] = yv;
+      d = fma(yv, pv[o], d);
+    }
+    if (USER) {
+      const double ybv = fma((double)Gn[e], vbias, wave_sum_f64(ybp));
+      if (lane == 0) {
+        yb[e] = ybv;
+        d = fma(ybv, vbias, d);
+      }
+    }
+    dsum += wave_sum_f64(d);
+    __builtin_amdgcn_wave_barrier();
+  }
+  const double tot = block_sum_f64<256>(lane == 0 ? dsum : 0.0, sh);
+  if (fst) store_partial(partials, tot);
+  else if (threadIdx.x == 0) partials[blockIdx.x] = tot;
+  if (fst && phase == CG_ALPHA) last_block_finalize(fst, CG_ALPHA, partials, nullptr, 0, sh);
+}
+
 int launch_cg_matvec(hipStream_t s, bool user_side, const CgState* st,
                      int update_p, int64_t E, int k, const float* G,
                      const float* Gs, const float* Gn, double* v, double* vb,
                      const double* r, const double* rb, double* y, double* yb,
                      double* partials, int n_part, CgState* fst, int phase) {
   if (n_part <= 0) return 0;
+  if (k > kMaxK) {
+    const int NP = ldk_of(k);
+    const size_t lds = (size_t)MV_WAVES * (3 * NP + 256) * sizeof(double);
+    if (user_side) {
+      MR_HIP(hipFuncSetAttribute((const void*)cg_matvec_largek_kernel<true>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      MR_LAUNCH(cg_matvec_largek_kernel<true>, dim3(n_part), dim3(256), lds, s, st, update_p, E,
+                k, G, Gs, Gn, v, vb, r, rb, y, yb, partials, fst, phase);
+    } else {
+      MR_HIP(hipFuncSetAttribute((const void*)cg_matvec_largek_kernel<false>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      MR_LAUNCH(cg_matvec_largek_kernel<false>, dim3(n_part), dim3(256), lds, s, st, update_p, E,
+                k, G, Gs, Gn, v, vb, r, rb, y, yb, partials, fst, phase);
+    }
+    MR_HIP(hipGetLastError());
+    return 0;
+  }
 #define MR_MV_CASE(NB)                                                                   \
   case NB:                                                                               \
     if (user_side)                                                                       \
@@ -1773,6 +2085,7 @@ int launch_solve(hipStream_t s, bool user_side, int64_t E, int k, double ridge,
                  const float* C, const float* Cb, float* x, float* xb,
                  int* nonpd) {
   if (E <= 0) return 0;
+  MR_CHECK(k <= kMaxK, "the exact (Cholesky) solver holds K x K in LDS: k <= 128");
   const int K = user_side ? k + 1 : k;
   const size_t lds = (size_t)(K * K + K) * sizeof(double);
   if (user_side) {

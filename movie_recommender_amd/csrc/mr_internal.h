@@ -76,7 +76,8 @@ extern thread_local Stager t_stager;
     if (::mr::t_stager.d2h((s), (dst), (src), (size_t)(bytes))) return -1; \
   } while (0)
 
-constexpr int kMaxK = 128;        // largest factor count the Gram kernel tiles
+constexpr int kMaxK = 128;        // largest k of the register-tiled (MFMA) Gram and GEMV kernels
+constexpr int kMaxKLarge = 512;   // k > 128: streamed large-k kernels (gram_largek_kernel, ...)
 constexpr int kMfmaMinK = 32;     // k < 32: VALU Gram (gram_valu_kernel), no fused CG start
 // Row stride of factor tables / CG vectors: k rounded up to a multiple of 16
 // (one 16-wide block of the tri16 storage), so every Gram lane's NB-float segment of a row

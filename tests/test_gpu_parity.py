@@ -25,13 +25,15 @@ pytestmark = pytest.mark.gpu
 DENSE = ["als_dense_38x45_k5.npz", "als_dense_40x45_k3.npz",
          "als_dense_300x200_k10.npz", "als_dense_200x150_k32.npz",
          "als_dense_60x50_k32_it3.npz", "als_dense_300x260_k64.npz",
-         "als_dense_400x300_k128.npz"]
+         "als_dense_400x300_k128.npz", "als_dense_340x300_k144.npz"]
 MLSHAPE = ["als_mlshape_k10_it2.npz", "als_mlshape_k10_it4.npz",
            "als_mlshape_k32_it2.npz", "als_mlshape_k32_it4.npz",
            "als_mlshape_k64_it2.npz", "als_mlshape_k64_it4.npz"]
-# headline-k fixtures: NB = 4 / 8 block GEMV and the fused CG start
+# headline-k fixtures: NB = 4 / 8 block GEMV and the fused CG start; k = 144
+# runs the streamed large-k Gram / GEMV (split work items at chunk 64)
 HEADLINE = ["als_dense_60x50_k32_it3.npz", "als_dense_300x260_k64.npz",
-            "als_dense_400x300_k128.npz", "als_mlshape_k64_it4.npz"]
+            "als_dense_400x300_k128.npz", "als_mlshape_k64_it4.npz",
+            "als_dense_340x300_k144.npz"]
 
 
 def max_iteration_of(name, d):
@@ -224,11 +226,12 @@ def test_replay_from_snapshot_is_bitwise_identical(gpu):
         assert np.array_equal(U, U1) and np.array_equal(V, V1)
 
 
-@pytest.mark.parametrize("k", [3, 10, 16, 20, 32, 33, 64, 65, 96, 128])
+@pytest.mark.parametrize("k", [3, 10, 16, 20, 32, 33, 64, 65, 96, 128, 144, 200])
 def test_gram_kernel_vs_numpy(gpu, k):
-    """Normal equations of both sides (bf16x3 split on the bf16 MFMA) against
-    fp64 NumPy, including heavy entities split across waves (chunk 64 forces
-    slabs) and empty entities."""
+    """Normal equations of both sides against fp64 NumPy -- VALU fp32 for
+    k < 32, bf16x3 split on the bf16 MFMA for 32 <= k <= 128, the streamed
+    large-k kernel above -- including heavy entities split across waves
+    (chunk 64 forces slabs) and empty entities."""
     from movie_recommender_amd.engine import AlsContext
     from oracle import als_oracle as O
     rng = np.random.default_rng(k)
@@ -258,7 +261,7 @@ def test_gram_kernel_vs_numpy(gpu, k):
     _lib.check(_lib.lib().mr_set_gram_chunk(2048), "reset chunk")
 
 
-@pytest.mark.parametrize("k", [5, 10, 32, 33, 64, 65, 128])
+@pytest.mark.parametrize("k", [5, 10, 32, 33, 64, 65, 128, 144, 200])
 @pytest.mark.parametrize("fuse,chunk", [(1, 2048), (1, 64), (0, 2048)])
 def test_cg_iterations_vs_oracle(gpu, k, fuse, chunk):
     """The first CG iterations of both sides -- CG start (fused in the Gram
