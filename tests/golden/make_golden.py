@@ -258,24 +258,28 @@ def g6():
 
 
 def g7():
-    """k > 128 (round 2): the streamed large-k Gram and block GEMV (NB = 9:
-    four folded diagonal pairs plus an odd last block) pinned to the
-    reference on a dense fixture."""
-    name, (nu, ni, k, dseed, iseed, mi) = ("als_dense_340x300_k144.npz", (340, 300, 144, 9, 3, 3))
-    u, i, r, tu, ti, tr = synth.dense_fixture(nu, ni, k, 0.8, seed=dseed)
-    U0, V0 = ref.init_factors(nu, ni, k, iseed)
-    res = {}
-    for tc in (8, 1):
-        ref.set_thread_count(tc)
-        res[tc] = ref.als(u, i, r, k, U0, V0, max_iteration=mi)
-    U, V, ret = res[8]
-    spread = max(np.max(np.abs(res[1][0] - U)) / np.max(np.abs(U)),
-                 np.max(np.abs(res[1][1] - V)) / np.max(np.abs(V)))
-    np.savez_compressed(os.path.join(HERE, name), user_ids=u, item_ids=i, ratings=r,
-                        k=k, num_users=nu, num_items=ni, max_iteration=mi,
-                        U0=U0, V0=V0, U=U, V=V, ret=ret, ret_tc1=res[1][2],
-                        tc_spread=spread, meta=json.dumps(_meta(8)))
-    print("G7", name, "N", len(r), "ret", ret, "tc1 ret", res[1][2], "spread", spread, flush=True)
+    """Round 2: the streamed large-k Gram and block GEMV (k = 144, NB = 9:
+    four folded diagonal pairs plus an odd last block) and the VALU Gram of
+    k < 32 (k = 24, NB = 2) pinned to the reference on dense fixtures."""
+    for name, (nu, ni, k, dseed, iseed, mi) in (
+            ("als_dense_340x300_k144.npz", (340, 300, 144, 9, 3, 3)),
+            # k = 24: the NB = 2 VALU Gram (k < 32) with a folded diagonal pair
+            ("als_dense_120x100_k24.npz", (120, 100, 24, 11, 3, 200))):
+        u, i, r, tu, ti, tr = synth.dense_fixture(nu, ni, k, 0.8, seed=dseed)
+        U0, V0 = ref.init_factors(nu, ni, k, iseed)
+        res = {}
+        for tc in (8, 1):
+            ref.set_thread_count(tc)
+            res[tc] = ref.als(u, i, r, k, U0, V0, max_iteration=mi)
+        U, V, ret = res[8]
+        spread = max(np.max(np.abs(res[1][0] - U)) / np.max(np.abs(U)),
+                     np.max(np.abs(res[1][1] - V)) / np.max(np.abs(V)))
+        np.savez_compressed(os.path.join(HERE, name), user_ids=u, item_ids=i, ratings=r,
+                            k=k, num_users=nu, num_items=ni, max_iteration=mi,
+                            U0=U0, V0=V0, U=U, V=V, ret=ret, ret_tc1=res[1][2],
+                            tc_spread=spread, meta=json.dumps(_meta(8)))
+        print("G7", name, "N", len(r), "ret", ret, "tc1 ret", res[1][2], "spread", spread,
+              flush=True)
     ref.set_thread_count(1)
 
 

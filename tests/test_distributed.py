@@ -102,7 +102,8 @@ def test_sharded_algorithm_gloo_cpu(tmp_path, fixture, max_it):
 @pytest.mark.gpu
 @pytest.mark.parametrize("fixture,max_it", [("als_dense_300x200_k10.npz", 200),
                                             ("als_dense_300x260_k64.npz", 200),
-                                            ("als_mlshape_k64_it4.npz", 4)])
+                                            ("als_mlshape_k64_it4.npz", 4),
+                                            ("als_dense_340x300_k144.npz", 3)])
 def test_engine_two_ranks_gloo_matches_single(gpu, tmp_path, fixture, max_it):
     """The real engine sharded over 2 ranks (both on cuda:0 on a one-GPU box;
     cost-balanced shards, all-reduced CG scalars, all-gathered factor shards)

@@ -25,7 +25,8 @@ pytestmark = pytest.mark.gpu
 DENSE = ["als_dense_38x45_k5.npz", "als_dense_40x45_k3.npz",
          "als_dense_300x200_k10.npz", "als_dense_200x150_k32.npz",
          "als_dense_60x50_k32_it3.npz", "als_dense_300x260_k64.npz",
-         "als_dense_400x300_k128.npz", "als_dense_340x300_k144.npz"]
+         "als_dense_400x300_k128.npz", "als_dense_340x300_k144.npz",
+         "als_dense_120x100_k24.npz"]
 MLSHAPE = ["als_mlshape_k10_it2.npz", "als_mlshape_k10_it4.npz",
            "als_mlshape_k32_it2.npz", "als_mlshape_k32_it4.npz",
            "als_mlshape_k64_it2.npz", "als_mlshape_k64_it4.npz"]
