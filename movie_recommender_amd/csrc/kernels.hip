@@ -415,10 +415,9 @@ __host__ __device__ constexpr int acc_tile(int bi, int bj, int nb) {
 // through LDS -- a DPP tree cost 4x the instructions), column products
 // B^T v_bi to y_bj (summed over the 4 rows by lane shuffles), both in a
 // fixed order; a diagonal block contributes its stored triangle only.
-// Two passes (block rows, then block columns) with one tile's fp64 copy live
-// at a time: this epilogue must fit the main loop's register budget (3 waves
-// per SIMD at k = 64), so tile conversions are not hoisted
-// (sched_barrier).  v in sc.pv (virtual order).  Returns y at virtual
+// One tile's fp64 copy live at a time: this epilogue must fit the main
+// loop's register budget (3 waves per SIMD at k = 64), so tile conversions
+// are not hoisted (sched_barrier).  v in sc.pv (virtual order).  Returns y at virtual
 // o = lane + 64 h in yo[h] (without the bias column) -- 0 for padding.
 template <int NB>
 __device__ __forceinline__ void acc_matvec(const floatx4 (&acc)[NB * (NB + 1) / 2],
@@ -426,11 +425,23 @@ __device__ __forceinline__ void acc_matvec(const floatx4 (&acc)[NB * (NB + 1) / 
                                            double (&yo)[(16 * NB + 63) / 64]) {
   constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
   const int lane = threadIdx.x & 63, q = lane >> 4, col = lane & 15;
-  // pass 1: row products y_bi[4q + r] = sum_bj B(bi,bj)[4q + r][:] v_bj
+  // One pass over the upper tiles, block rows in order, each row starting at
+  // its diagonal block: every accumulator is converted to fp64 once and feeds
+  // both its row product y_bi[4q + r] += B(bi,bj)[4q + r][col] v_bj[col]
+  // (lane partials, summed over the 16 lanes of row group q through LDS) and
+  // its column product y_bj[col] += B(bi,bj)[4q + r][col] v_bi[4q + r] (a
+  // per-lane running sum per block column, contributions in bi order --
+  // column bi is complete once row bi is done).
+  double cc[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) cc[b] = 0.0;
 #pragma unroll
   for (int bi = 0; bi < NB; ++bi) {
     const bool lower = (bi & 1) && !((NB & 1) && bi == NB - 1);
     double R[4] = {0.0, 0.0, 0.0, 0.0};
+    const double2 va = *reinterpret_cast<const double2*>(&sc.pv[16 * bi + 4 * q]);
+    const double2 vb = *reinterpret_cast<const double2*>(&sc.pv[16 * bi + 4 * q + 2]);
+    const double vr[4] = {va.x, va.y, vb.x, vb.y};   // v_bi at rows 4q + r
 #pragma unroll
     for (int bj = bi; bj < NB; ++bj) {
       const int t = acc_tile(bi, bj, NB);
@@ -438,39 +449,23 @@ __device__ __forceinline__ void acc_matvec(const floatx4 (&acc)[NB * (NB + 1) / 
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = 4 * q + r;
+        const double a = (double)acc[t][r];
         // diagonal block: the bf16x3 sum is not bitwise symmetric, so use
         // exactly the triangle tri16 stores (upper for even blocks and the
-        // odd last block, lower + side diagonal for odd folded blocks)
-        const bool use = bi != bj || (lower ? (col <= row) : (col >= row));
-        R[r] = fma(use ? (double)acc[t][r] : 0.0, vj, R[r]);
+        // odd last block, lower + side diagonal for odd folded blocks); the
+        // column product skips the diagonal element the row product used
+        const bool use_r = bi != bj || (lower ? (col <= row) : (col >= row));
+        const bool use_c = bi != bj || (lower ? (col < row) : (col > row));
+        R[r] = fma(use_r ? a : 0.0, vj, R[r]);
+        cc[bj] = fma(use_c ? a : 0.0, vr[r], cc[bj]);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) sc.partR[4 * bi + r][lane] = R[r];
-  }
-  // pass 2: column products y_bj[col] = sum_{bi <= bj} B(bi,bj)[:][col] . v_bi
-#pragma unroll
-  for (int bj = 0; bj < NB; ++bj) {
-    const bool lower = (bj & 1) && !((NB & 1) && bj == NB - 1);
-    double c = 0.0;
-#pragma unroll
-    for (int bi = 0; bi <= bj; ++bi) {
-      const int t = acc_tile(bi, bj, NB);
-      const double2 va = *reinterpret_cast<const double2*>(&sc.pv[16 * bi + 4 * q]);
-      const double2 vb = *reinterpret_cast<const double2*>(&sc.pv[16 * bi + 4 * q + 2]);
-      const double vr[4] = {va.x, va.y, vb.x, vb.y};   // v_bi at rows 4q + r
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 4 * q + r;
-        const bool use = bi != bj || (lower ? (col < row) : (col > row));
-        c = fma(use ? (double)acc[t][r] : 0.0, vr[r], c);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    c = xor_sum_f64<16>(c);
+    double c = xor_sum_f64<16>(cc[bi]);
     c = xor_sum_f64<32>(c);   // identical in all 4 rows
-    if (q == 0) sc.yC[16 * bj + col] = c;
+    if (q == 0) sc.yC[16 * bi + col] = c;
   }
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
