@@ -209,3 +209,43 @@ def build_similar_movies(movie_genres, movie_ratings, buff_point, buff_limit, nu
             if oc[m]:
                 out[int(f._ids[m])] = [int(x) for x in f._ids[oj[m, :oc[m]]]]
         return out
+
+
+# --------------------------------------------------------------------------
+# Movie-movie cosine similarity on the ALS factor layout (north star: "the
+# movie-movie cosine-similarity pass reuses the same factor layout")
+# --------------------------------------------------------------------------
+def similar_by_factors(num_factors, als_movie_factors, als_movie_ids, num_results=20,
+                       query=None, device=0):
+    """For each query movie (standard ids; all of ``als_movie_ids`` when None)
+    the ``num_results`` other movies with the highest cosine similarity of
+    their ALS factor rows (``als{k}_item_factors`` / ``als{k}_movie_ids``,
+    the reference's objects, ``recommend.py:62-70``).  Returns
+    ``{movie_id: [(cosine, movie_id), ...]}``, ordered by (cosine, movie id)
+    descending.
+
+    Runs on the serving path's kernels: the rows are normalised on the host
+    (fp64), the candidate table holds the normalised rows with zero medians and
+    each query is a "user" row (normalised factors, zero bias), so the score
+    kernel's fp64 expression ``s = 0; s += x_i * v_i ...`` IS the cosine, and
+    the exact top-N select (self excluded) ranks it.  A zero factor row has
+    cosine 0 with everything."""
+    from .serving import MovieTable
+    k = int(num_factors)
+    V = numpy.ascontiguousarray(als_movie_factors, dtype=numpy.float64).reshape(-1, k)
+    norm = numpy.sqrt(numpy.sum(V * V, axis=1))
+    Vn = V / numpy.where(norm > 0, norm, 1.0)[:, None]
+    zero_medians = {m: 0.0 for m in als_movie_ids}
+    qids = list(als_movie_ids) if query is None else list(query)
+    X = numpy.zeros((len(qids), k + 1))
+    for t, m in enumerate(qids):
+        X[t, :k] = Vn[als_movie_ids[m]]
+    out = {}
+    with MovieTable(k, Vn, als_movie_ids, zero_medians, device) as table:
+        step = 4096
+        for s in range(0, len(qids), step):
+            chunk = qids[s:s + step]
+            lists = table.top_n(X[s:s + step], [[m] for m in chunk], num_results)
+            for m, lst in zip(chunk, lists):
+                out[m] = lst
+    return out

@@ -404,6 +404,36 @@ def test_band_realistic_heldout_rmse(gpu):
     assert lo <= np.mean(vals) <= hi, (vals, lo, hi)
 
 
+def test_band_headline_shape_heldout_rmse(gpu):
+    """G4 at the headline shape: MovieLens-full-shaped synthetic data, k = 64,
+    4 ALS iterations; the mean held-out RMSE of 3 seeds must fall inside the
+    compiled reference's band (3 seeds x thread counts 4, 8; min - 3 sd ..
+    max + 3 sd), band_mlfull_k64.json from tests/golden/make_golden.py g8."""
+    from movie_recommender_amd import synth
+    from movie_recommender_amd.engine import AlsContext
+    from oracle import als_oracle as O
+    from oracle.ref import init_factors
+    with open(os.path.join(GOLDEN, "band_mlfull_k64.json")) as f:
+        band = json.load(f)
+    k, mi = band["k"], band["max_iteration"]
+    rs = synth.movielens_like(band["shape"], k, seed=band["data_seed"],
+                              test_ratio=band["test_ratio"])
+    assert rs.n == band["n_train"] and abs(float(np.sum(rs.ratings)) - band["ratings_checksum"]) < 1e-6
+    lo = band["test_rmse_min"] - 3 * band["test_rmse_std"]
+    hi = band["test_rmse_max"] + 3 * band["test_rmse_std"]
+    vals = []
+    for seed in range(3):
+        U0, V0 = init_factors(rs.num_users, rs.num_items, k, seed)
+        with AlsContext(rs.user_ids, rs.item_ids, rs.ratings, k, rs.num_users,
+                        rs.num_items) as ctx:
+            ctx.set_factors(U0, V0)
+            ctx.run(0.01, mi)
+            U, V = ctx.get_factors()
+        vals.append(O.rmse(U, V, rs.test_user_ids, rs.test_item_ids, rs.test_ratings, k))
+        print(f"seed {seed}: held-out RMSE {vals[-1]:.5f} (band {lo:.5f} .. {hi:.5f})", flush=True)
+    assert lo <= np.mean(vals) <= hi, (vals, lo, hi)
+
+
 def test_predict_matches_reference_formula(gpu):
     from movie_recommender_amd.engine import AlsContext
     from oracle import als_oracle as O
