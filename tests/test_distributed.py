@@ -99,6 +99,21 @@ def test_sharded_algorithm_gloo_cpu(tmp_path, fixture, max_it):
     assert rel_err(U, d["U"]) < max(1e-6, tol) and rel_err(V, d["V"]) < max(1e-6, tol)
 
 
+def test_sharded_algorithm_gloo_cpu_world3(tmp_path):
+    """World size 3 (uneven, cost-balanced shards; 3 all-gather pieces and a
+    3-way scalar all-reduce) on CPU against the single-process algorithm."""
+    from oracle import als_oracle as O
+    fixture = "als_dense_300x200_k10.npz"
+    d = load_golden(fixture)
+    k = int(d["k"])
+    U, V, ret = run_workers("oracle", fixture, 3, tmp_path, 200)
+    Uo, Vo, reto, _ = O.als_block(d["user_ids"], d["item_ids"], d["ratings"], k, d["U0"],
+                                  d["V0"], max_iteration=200)
+    assert ret == reto == int(d["ret"])
+    tol = max(1e-9, 20 * float(d["tc_spread"]))
+    assert rel_err(U, Uo) < tol and rel_err(V, Vo) < tol
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("fixture,max_it", [("als_dense_300x200_k10.npz", 200),
                                             ("als_dense_300x260_k64.npz", 200),
