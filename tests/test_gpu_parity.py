@@ -96,8 +96,9 @@ def test_headline_paths_golden(gpu, name, chunk, fuse):
     """Every CG start path against the compiled reference at k = 32 / 64 /
     128: the Gram-epilogue start (fuse 1), the start of split entities after
     slab_reduce (chunk 64 splits every entity), and the unfused reference
-    order (fuse 0: x -> matvec -> INIT update).  Speculative launches on and
-    off must give identical CG counts and bitwise-identical factors."""
+    order (fuse 0: x -> matvec -> INIT update).  Every launch-ahead level
+    (MR_OPT_CG_SPECULATE 0, 1, 2) must give identical CG counts and
+    bitwise-identical factors."""
     from movie_recommender_amd.engine import AlsContext
     from movie_recommender_amd import _lib
     d = load_golden(name)
@@ -105,7 +106,7 @@ def test_headline_paths_golden(gpu, name, chunk, fuse):
     mi = max_iteration_of(name, d)
     outs = []
     try:
-        for spec in (1, 0):
+        for spec in (1, 0, 2):
             with AlsContext(d["user_ids"], d["item_ids"], d["ratings"], k, nU, nI,
                             gram_chunk=chunk) as ctx:
                 ctx.set_option("fuse_start", fuse)
@@ -121,9 +122,9 @@ def test_headline_paths_golden(gpu, name, chunk, fuse):
     tol = tolerance_of(d)
     assert rel_err(U, d["U"]) <= tol, rel_err(U, d["U"])
     assert rel_err(V, d["V"]) <= tol, rel_err(V, d["V"])
-    (U2, V2), ret2, cu2, ci2 = outs[1]
-    assert (ret2, cu2, ci2) == (ret, cu, ci)
-    assert np.array_equal(U, U2) and np.array_equal(V, V2)
+    for (U2, V2), ret2, cu2, ci2 in outs[1:]:   # launch-ahead levels 0 and 2
+        assert (ret2, cu2, ci2) == (ret, cu, ci)
+        assert np.array_equal(U, U2) and np.array_equal(V, V2)
 
 
 def test_cg_least_squares_golden(gpu):
