@@ -237,6 +237,9 @@ def similar_by_factors(num_factors, als_movie_factors, als_movie_ids, num_result
     Vn = V / numpy.where(norm > 0, norm, 1.0)[:, None]
     zero_medians = {m: 0.0 for m in als_movie_ids}
     qids = list(als_movie_ids) if query is None else list(query)
+    missing = [m for m in qids if m not in als_movie_ids]
+    if missing:
+        raise ValueError(f"query movies without ALS factors: {missing[:5]}")
     X = numpy.zeros((len(qids), k + 1))
     for t, m in enumerate(qids):
         X[t, :k] = Vn[als_movie_ids[m]]
