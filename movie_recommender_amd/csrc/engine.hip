@@ -680,17 +680,31 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr, bool start
   }
 
   std::vector<int> seq_of;   // publish seq of iteration t's BETA step
-  auto launch_iter = [&](int t) -> int {
+  // One CG iteration t = head(t) + tail(t):
+  //   head(t): matvec (skipped for t = 0 after a fused start), sharded: its
+  //            p.Ap all-reduce; with sharding the matvec of t >= 1 also
+  //            applies and publishes the BETA step of t-1 (no finalize)
+  //   tail(t): update (+ BETA / publish in its last block when unsharded),
+  //            sharded: its r.r all-reduce
+  // Heads and tails are always enqueued alternately.
+  int heads = 0, tails = 0;
+  auto launch_head = [&]() -> int {
+    const int t = heads++;
+    if (started && t == 0) return 0;   // a fused start has done iteration 0's matvec
     hipEvent_t ev = nullptr;
-    if (!(started && t == 0)) {   // a fused start has done iteration 0's matvec
-      if (tic(mv_cls, t, &ev)) return -1;
-      if (launch_cg_matvec(stream, user, d_state, t > 0, S.E, k, S.G, S.Gs, S.Gn, S.p, S.pb,
-                           S.r, S.rb, S.q, S.qb, partials, S.n_part_mv, fst, CG_ALPHA))
-        return -1;
-      if (toc(mv_cls, t, ev)) return -1;
-      cur_parts = S.n_part_mv;
-      if (shard && allreduce_state_slot()) return -1;
-    }
+    if (tic(mv_cls, t, &ev)) return -1;
+    const int bseq = (shard && t > 0) ? seq_of[t - 1] : 0;
+    if (launch_cg_matvec(stream, user, d_state, t > 0, S.E, k, S.G, S.Gs, S.Gn, S.p, S.pb,
+                         S.r, S.rb, S.q, S.qb, partials, S.n_part_mv, fst, CG_ALPHA,
+                         d_mirror, bseq))
+      return -1;
+    if (toc(mv_cls, t, ev)) return -1;
+    cur_parts = S.n_part_mv;
+    return shard ? allreduce_state_slot() : 0;
+  };
+  auto launch_tail = [&]() -> int {
+    const int t = tails++;
+    hipEvent_t ev = nullptr;
     seq_of.push_back(++mirror_seq);
     if (tic(MR_K_CG_UPDATE, t, &ev)) return -1;
     if (launch_cg_update(stream, d_state, UPD_STEP, n, nb, xf, S.r, S.p, S.q, S.C, xb, S.rb,
@@ -698,10 +712,30 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr, bool start
       return -1;
     if (toc(MR_K_CG_UPDATE, t, ev)) return -1;
     cur_parts = kUpdParts;
-    return shard ? finalize_sharded(CG_BETA, seq_of.back()) : 0;
+    return shard ? allreduce_state_slot() : 0;
+  };
+  // Enqueue the alternating sequence until `nh` heads are out (tails follow
+  // their heads; no tail past max_it - 1, no head past max_it).
+  auto enqueue_to = [&](int nh) -> int {
+    while (heads < nh && heads <= max_it) {
+      if (tails < heads) {
+        if (tails >= max_it) break;
+        if (launch_tail()) return -1;
+      }
+      if (heads <= tails && launch_head()) return -1;
+    }
+    return 0;
+  };
+  // State t is published by tail(t) unsharded, by head(t+1) sharded.
+  const int lag = shard ? 1 : 0;
+  auto enqueue_iterations = [&](int n_it) -> int {   // iterations 0 .. n_it-1 complete
+    if (enqueue_to(n_it)) return -1;
+    while (tails < n_it && tails < max_it)
+      if (launch_tail()) return -1;
+    return 0;
   };
 
-  // Host protocol.  Iteration t publishes the state after it (BETA step)
+  // Host protocol.  Iteration t publishes the state after it (its BETA step)
   // under seq_of[t]; the host always reads the state of an EXACT iteration
   // (ring slot), so every decision below is a function of states that are
   // bitwise identical on all ranks of a sharded run (they derive from the
@@ -710,28 +744,23 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr, bool start
   // starts at 0), so iterations 0 and 1 are enqueued behind the start without
   // waiting (no-ops if the start already finished the solve).  Afterwards,
   // with the exact state S after iteration t known and not done:
-  //   * iteration t+1 is in flight (launched if it was not);
+  //   * iteration t+1 is in flight (launched if it was not), and so is what
+  //     publishes its state (sharded: the head of t+2);
   //   * iteration t+2 is enqueued too when S proves t+1 cannot stop
   //     (fails == 0, rr far above 1e-6, t+2 < max_it) -- the stream stays
-  //     busy while the host waits for the state after t+1;
-  //   * iteration t+1 publishes (S not done => it is not a no-op).
+  //     busy while the host waits for the state after t+1.
   const int spec = speculate;
-  int launched = 0;          // iterations enqueued so far
-  for (; launched < std::min(spec ? 2 : 1, max_it); ++launched)
-    if (launch_iter(launched)) return -1;
+  if (enqueue_iterations(std::min(spec ? 2 : 1, max_it))) return -1;
   CgMirror ms{};
   if (wait_mirror(seq_init, &ms)) return -1;
   int known = -1;            // ms = exact state after iteration `known` (-1: the start)
   while (!ms.done) {
-    if (launched == known + 1) {
-      if (launch_iter(launched)) return -1;
-      ++launched;
-    }
-    if (spec && launched == known + 2 && known + 2 < max_it &&
+    if (enqueue_iterations(known + 2)) return -1;
+    if (spec && known + 2 < max_it &&
         (spec >= 2 || (ms.fails == 0 && ms.rr > 1e-4))) {
-      if (launch_iter(launched)) return -1;
-      ++launched;
+      if (enqueue_iterations(known + 3)) return -1;
     }
+    if (lag && enqueue_to(known + 3)) return -1;   // the publisher of state known+1
     if (wait_mirror(seq_of[known + 1], &ms)) return -1;
     ++known;
     MR_CHECK(known <= max_it, "CG did not terminate");

@@ -1432,6 +1432,27 @@ __device__ __forceinline__ void publish(const CgScalars& v, CgMirror* ring, int 
   __hip_atomic_store(&m->seq, 2 * seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// BETA rule (matrix.cpp:507-525) on rr2 = r.r after the update: beta, the
+// two-strikes stagnation test, it++ and the loop-top stop tests.
+__device__ __forceinline__ void apply_beta(CgScalars& v, double rr2) {
+  v.final_rr = rr2;
+  const double beta = rr2 / v.rr;
+  v.beta = beta;
+  if (beta > 1.0 - v.min_dec) v.fails += 1;
+  else v.fails = 0;
+  if (v.fails >= 2) {
+    v.done = 1;
+    v.ret = v.it;
+  } else {
+    v.rr = rr2;
+    v.it += 1;
+    if (v.it >= v.max_it || rr2 < 1e-6) {
+      v.done = 1;
+      v.ret = v.it;
+    }
+  }
+}
+
 // INIT / ALPHA / BETA rules on the reduced sum s (one thread).
 __device__ void cg_finalize(CgState* st, int phase, double s, CgMirror* mirror, int seq) {
   CgScalars v = load_state(st);
@@ -1450,26 +1471,34 @@ __device__ void cg_finalize(CgState* st, int phase, double s, CgMirror* mirror, 
     v.n_matvec += 1;
     store_state(st, v);
   } else {
-    const double rr2 = s;
-    v.final_rr = rr2;
-    const double beta = rr2 / v.rr;
-    v.beta = beta;
-    if (beta > 1.0 - v.min_dec) v.fails += 1;
-    else v.fails = 0;
-    if (v.fails >= 2) {
-      v.done = 1;
-      v.ret = v.it;
-    } else {
-      v.rr = rr2;
-      v.it += 1;
-      if (v.it >= v.max_it || rr2 < 1e-6) {
-        v.done = 1;
-        v.ret = v.it;
-      }
-    }
+    apply_beta(v, s);
     store_state(st, v);
     publish(v, mirror, seq);
   }
+}
+
+// Sharded runs: the BETA step of iteration t (its r.r all-reduced into
+// comm[0]) is applied by the matvec of iteration t+1 instead of a one-block
+// finalize launch.  Every block derives beta and the stop decision from the
+// same state and comm[0] (a pure function, so all blocks agree: if it ends
+// the solve they skip the products); the last-arriving block -- every other
+// block has finished reading the state by then -- stores the new state,
+// publishes it under beta_seq and leaves its own p.Ap partial sum in comm[0]
+// for the next all-reduce.
+__device__ __forceinline__ bool matvec_entry(const CgState* st, int beta_seq, double& beta,
+                                             bool& skip) {
+  skip = false;
+  if (beta_seq > 0) {
+    CgScalars v = load_state(st);
+    if (v.done) return false;   // ended earlier (and published then)
+    apply_beta(v, v.comm0);
+    beta = v.beta;
+    skip = v.done != 0;
+    return true;
+  }
+  if (ald(&st->done)) return false;
+  beta = ald(&st->beta);
+  return true;
 }
 
 // Fused control: every block stores its partial sum write-through (sc1) and
@@ -1481,6 +1510,33 @@ __device__ void cg_finalize(CgState* st, int phase, double s, CgMirror* mirror, 
 __device__ __forceinline__ void store_partial(double* partials, double tot) {
   if (threadIdx.x == 0)
     __hip_atomic_store(&partials[blockIdx.x], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Last block of a sharded matvec that folds the previous BETA step: apply
+// it (the same decision every block took), publish, then leave the local
+// p.Ap sum in comm[0].
+__device__ void last_block_beta(CgState* st, double* partials, CgMirror* mirror, int seq,
+                                double* sh) {
+  __shared__ int s_last;
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_last = __hip_atomic_fetch_add(&st->arrive, 1u, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x)
+    acc += __hip_atomic_load(&partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const double tot = block_sum_f64<256>(acc, sh);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(&st->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    CgScalars v = load_state(st);
+    apply_beta(v, v.comm0);
+    v.comm0 = tot;
+    store_state(st, v);
+    publish(v, mirror, seq);
+  }
 }
 
 __device__ void last_block_finalize(CgState* st, int phase, double* partials, CgMirror* mirror,
@@ -1522,18 +1578,19 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 4 : 1)) void cg_matvec_kernel(
     const float* __restrict__ Gn, double* __restrict__ v, double* __restrict__ vb,
     const double* __restrict__ r, const double* __restrict__ rb,
     double* __restrict__ y, double* __restrict__ yb, double* __restrict__ partials,
-    CgState* fst, int phase) {
-  if (ald(&st->done)) return;
+    CgState* fst, int phase, CgMirror* mirror, int beta_seq) {
+  double beta = 0.0;
+  bool skip;
+  if (!matvec_entry(st, beta_seq, beta, skip)) return;
   constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2, NTILE = NO + NF + (NB & 1);
   constexpr int64_t GS = (int64_t)NTILE * 256 + NF * 16;   // == gsize_of(k)
   constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
   __shared__ MvScratch<NB> scr[MV_WAVES];
   __shared__ double sh[MV_WAVES];
-  const double beta = ald(&st->beta);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   MvScratch<NB>& sc = scr[wid];
   double dsum = 0.0;
-  for (int64_t e = (int64_t)blockIdx.x * MV_WAVES + wid; e < E;
+  for (int64_t e = (int64_t)blockIdx.x * MV_WAVES + wid; e < (skip ? 0 : E);
        e += (int64_t)gridDim.x * MV_WAVES) {
     // issue order matters for the in-order vmcnt: vector loads first, then
     // every G block of this entity, so staging p waits only for the former
@@ -1603,7 +1660,10 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 4 : 1)) void cg_matvec_kernel(
   const double tot = block_sum_f64<256>(lane == 0 ? dsum : 0.0, sh);
   if (fst) store_partial(partials, tot);
   else if (threadIdx.x == 0) partials[blockIdx.x] = tot;
-  if (fst && phase == CG_ALPHA) last_block_finalize(fst, CG_ALPHA, partials, nullptr, 0, sh);
+  if (fst && phase == CG_ALPHA) {
+    if (beta_seq > 0) last_block_beta(fst, partials, mirror, beta_seq, sh);
+    else last_block_finalize(fst, CG_ALPHA, partials, nullptr, 0, sh);
+  }
 }
 
 // K2 for k > 128: the same block GEMV (fused p update, fp64 products, p.q
@@ -1618,8 +1678,10 @@ __global__ __launch_bounds__(256) void cg_matvec_largek_kernel(
     const float* __restrict__ G, const float* __restrict__ Gs, const float* __restrict__ Gn,
     double* __restrict__ v, double* __restrict__ vb, const double* __restrict__ r,
     const double* __restrict__ rb, double* __restrict__ y, double* __restrict__ yb,
-    double* __restrict__ partials, CgState* fst, int phase) {
-  if (ald(&st->done)) return;
+    double* __restrict__ partials, CgState* fst, int phase, CgMirror* mirror, int beta_seq) {
+  double beta = 0.0;
+  bool skip;
+  if (!matvec_entry(st, beta_seq, beta, skip)) return;
   extern __shared__ double lm_sm[];
   __shared__ double sh[MV_WAVES];
   const int NB = nb16_of(k), ldk = 16 * NB, NP = ldk;
@@ -1631,13 +1693,12 @@ __global__ __launch_bounds__(256) void cg_matvec_largek_kernel(
   double* yC = yR + NP;
   double* red = yC + NP;
   const int rr = lane >> 2, c4 = (lane & 3) * 4;
-  const double beta = ald(&st->beta);
   double dsum = 0.0;
   auto diag_tile = [&](int b, bool& lower) {
     lower = (b & 1) && b < 2 * NF;
     return (b < 2 * NF) ? NO + (b >> 1) : NO + NF;
   };
-  for (int64_t e = (int64_t)blockIdx.x * MV_WAVES + wid; e < E;
+  for (int64_t e = (int64_t)blockIdx.x * MV_WAVES + wid; e < (skip ? 0 : E);
        e += (int64_t)gridDim.x * MV_WAVES) {
     const float4* Ge = reinterpret_cast<const float4*>(G + e * GS);
     double* ve = v + e * ldk;
@@ -1738,14 +1799,18 @@ __global__ __launch_bounds__(256) void cg_matvec_largek_kernel(
   const double tot = block_sum_f64<256>(lane == 0 ? dsum : 0.0, sh);
   if (fst) store_partial(partials, tot);
   else if (threadIdx.x == 0) partials[blockIdx.x] = tot;
-  if (fst && phase == CG_ALPHA) last_block_finalize(fst, CG_ALPHA, partials, nullptr, 0, sh);
+  if (fst && phase == CG_ALPHA) {
+    if (beta_seq > 0) last_block_beta(fst, partials, mirror, beta_seq, sh);
+    else last_block_finalize(fst, CG_ALPHA, partials, nullptr, 0, sh);
+  }
 }
 
 int launch_cg_matvec(hipStream_t s, bool user_side, const CgState* st,
                      int update_p, int64_t E, int k, const float* G,
                      const float* Gs, const float* Gn, double* v, double* vb,
                      const double* r, const double* rb, double* y, double* yb,
-                     double* partials, int n_part, CgState* fst, int phase) {
+                     double* partials, int n_part, CgState* fst, int phase,
+                     CgMirror* mirror, int beta_seq) {
   if (n_part <= 0) return 0;
   if (k > kMaxK) {
     const int NP = ldk_of(k);
@@ -1754,12 +1819,12 @@ int launch_cg_matvec(hipStream_t s, bool user_side, const CgState* st,
       MR_HIP(hipFuncSetAttribute((const void*)cg_matvec_largek_kernel<true>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       MR_LAUNCH(cg_matvec_largek_kernel<true>, dim3(n_part), dim3(256), lds, s, st, update_p, E,
-                k, G, Gs, Gn, v, vb, r, rb, y, yb, partials, fst, phase);
+                k, G, Gs, Gn, v, vb, r, rb, y, yb, partials, fst, phase, mirror, beta_seq);
     } else {
       MR_HIP(hipFuncSetAttribute((const void*)cg_matvec_largek_kernel<false>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       MR_LAUNCH(cg_matvec_largek_kernel<false>, dim3(n_part), dim3(256), lds, s, st, update_p, E,
-                k, G, Gs, Gn, v, vb, r, rb, y, yb, partials, fst, phase);
+                k, G, Gs, Gn, v, vb, r, rb, y, yb, partials, fst, phase, mirror, beta_seq);
     }
     MR_HIP(hipGetLastError());
     return 0;
@@ -1768,11 +1833,12 @@ int launch_cg_matvec(hipStream_t s, bool user_side, const CgState* st,
   case NB:                                                                               \
     if (user_side)                                                                       \
       MR_LAUNCH((cg_matvec_kernel<NB, true>), dim3(n_part), dim3(256), 0, s, st, update_p, \
-                E, k, ldk_of(k), G, Gs, Gn, v, vb, r, rb, y, yb, partials, fst, phase);   \
+                E, k, ldk_of(k), G, Gs, Gn, v, vb, r, rb, y, yb, partials, fst, phase,    \
+                mirror, beta_seq);                                                       \
     else                                                                                 \
       MR_LAUNCH((cg_matvec_kernel<NB, false>), dim3(n_part), dim3(256), 0, s, st,         \
                 update_p, E, k, ldk_of(k), G, Gs, Gn, v, vb, r, rb, y, yb, partials, fst, \
-                phase);                                                                  \
+                phase, mirror, beta_seq);                                                \
     break;
   switch (nb16_of(k)) {
     MR_MV_CASE(1) MR_MV_CASE(2) MR_MV_CASE(3) MR_MV_CASE(4)

@@ -232,12 +232,15 @@ int launch_slab_reduce(hipStream_t s, bool user_side, int k,
 // Fused control (single-GPU runs): fst != nullptr makes the last block of
 // the matvec compute alpha (phase CG_ALPHA) and the last block of the update
 // apply the INIT / BETA rules and publish to `mirror` -- no control kernels.
+// Sharded runs: beta_seq > 0 makes the matvec first apply the previous
+// iteration's BETA rule (all-reduced r.r in comm[0]) and its last block
+// publish that state under beta_seq (no finalize launch).
 int launch_cg_matvec(hipStream_t s, bool user_side, const CgState* st,
                      int update_p, int64_t E, int k, const float* G,
                      const float* Gs, const float* Gn, double* v, double* vb,
                      const double* r, const double* rb, double* y, double* yb,
                      double* partials, int n_part, CgState* fst = nullptr,
-                     int phase = CG_INIT);
+                     int phase = CG_INIT, CgMirror* mirror = nullptr, int beta_seq = 0);
 // x is the fp32 factor table (and bias), r / p / q the fp64 CG vectors.
 int launch_cg_update(hipStream_t s, const CgState* st, int mode, int64_t n,
                      int64_t nb, float* x, double* r, double* p, const double* q,
