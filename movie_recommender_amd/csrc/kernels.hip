@@ -644,23 +644,42 @@ template <int T>
 __device__ __forceinline__ int row_bcast(int v) {
   return __builtin_amdgcn_mov_dpp(v, 0x150 + T, 0xF, 0xF, false);
 }
-template <int NB, int T>
+// Row source: a 64-bit base (any table size), or (BUF, tables < 2 GiB) a
+// buffer resource with a 32-bit byte offset -- one shift-or per row instead
+// of 64-bit address arithmetic; out-of-range offsets read 0.
+struct RowSrc {
+  const char* Fc;                 // 64-bit path: table + this lane's column offset
+  __amdgpu_buffer_rsrc_t rsrc;    // BUF path: whole table
+  uint32_t colb;                  // BUF path: this lane's column offset, bytes
+};
+template <int NB, int T, bool BUF>
 __device__ __forceinline__ void gather_row(float (&f)[8][NB], float (&w)[8], ChunkRegs cr,
-                                           const char* __restrict__ Fc, uint32_t row_bytes) {
+                                           const RowSrc& src, uint32_t row_bytes) {
   const int ri = row_bcast<T>(cr.idx);
   w[T] = __builtin_bit_cast(float, row_bcast<T>(__builtin_bit_cast(int, cr.w)));
-  load_row_seg<NB>(f[T], reinterpret_cast<const float*>(Fc + (uint64_t)(uint32_t)ri * row_bytes));
+  if constexpr (BUF) {
+    const uint32_t off = (uint32_t)ri * row_bytes + src.colb;
+#pragma unroll
+    for (int h = 0; h < NB / 4; ++h) {
+      const floatx4 v = __builtin_bit_cast(
+          floatx4, __builtin_amdgcn_raw_buffer_load_b128(src.rsrc, (int)(off + 16 * h), 0, 0));
+      f[T][4 * h] = v[0]; f[T][4 * h + 1] = v[1]; f[T][4 * h + 2] = v[2]; f[T][4 * h + 3] = v[3];
+    }
+  } else {
+    load_row_seg<NB>(f[T],
+                     reinterpret_cast<const float*>(src.Fc + (uint64_t)(uint32_t)ri * row_bytes));
+  }
 }
-template <int NB, int... T>
+template <int NB, bool BUF, int... T>
 __device__ __forceinline__ void gather_rows(float (&f)[8][NB], float (&w)[8], ChunkRegs cr,
-                                            const char* __restrict__ Fc, uint32_t row_bytes,
+                                            const RowSrc& src, uint32_t row_bytes,
                                             std::integer_sequence<int, T...>) {
-  (gather_row<NB, T>(f, w, cr, Fc, row_bytes), ...);
+  (gather_row<NB, T, BUF>(f, w, cr, src, row_bytes), ...);
 }
-template <int NB>
+template <int NB, bool BUF>
 __device__ __forceinline__ void gather_half(float (&f)[8][NB], float (&w)[8], ChunkRegs cr,
-                                            const char* __restrict__ Fc, uint32_t row_bytes) {
-  gather_rows<NB>(f, w, cr, Fc, row_bytes, std::make_integer_sequence<int, 8>{});
+                                            const RowSrc& src, uint32_t row_bytes) {
+  gather_rows<NB, BUF>(f, w, cr, src, row_bytes, std::make_integer_sequence<int, 8>{});
 }
 
 // rhs c = sum a w and (user side) row sums, fp32 on VALU, per lane over its
@@ -727,7 +746,7 @@ __device__ __forceinline__ void bf3_mfma(floatx4 (&acc)[NB * (NB + 1) / 2],
   }
 }
 
-template <int NB, bool USER, bool FUSE>
+template <int NB, bool USER, bool FUSE, bool BUF>
 __device__ __forceinline__ void gram_wave(
     int64_t wi, const WorkItem* __restrict__ work,
     const int32_t* __restrict__ idx, const float* __restrict__ val,
@@ -744,7 +763,13 @@ __device__ __forceinline__ void gram_wave(
   const int q = lane >> 4, col = lane & 15;
   const int64_t end = wbeg + wlen;
   constexpr uint32_t row_bytes = 64u * NB;     // ldk = 16 NB floats
-  const char* Fc = reinterpret_cast<const char*>(F) + 4 * NB * col;
+  RowSrc src;
+  src.Fc = reinterpret_cast<const char*>(F) + 4 * NB * col;
+  src.colb = 4u * NB * (uint32_t)col;
+  if constexpr (BUF)
+    src.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(F), (short)0,
+                                                 (int)((uint32_t)(zrow + 1) * row_bytes),
+                                                 0x00020000);
 
   // fused CG start: this lane's x entries (virtual (b, col) = natural
   // NB*col + b, contiguous) are fetched now and used after the loop
@@ -803,13 +828,13 @@ __device__ __forceinline__ void gram_wave(
   bias32(h1, 1);
   float Fr[8][NB], w[8];
   u32x4_t P[3][NB];
-  gather_half<NB>(Fr, w, fin32(h0, 0), Fc, row_bytes);
+  gather_half<NB, BUF>(Fr, w, fin32(h0, 0), src, row_bytes);
   bf3_split<NB, USER>(P, cacc, sacc, wsum, Fr, w);
   const int nhalves = (wlen + 31) >> 5;
   for (int h = 0; h < nhalves; ++h) {
     const ChunkRaw h3 = ld32(h + 3);
     bias32(h2, h + 2);
-    gather_half<NB>(Fr, w, fin32(h1, h + 1), Fc, row_bytes);
+    gather_half<NB, BUF>(Fr, w, fin32(h1, h + 1), src, row_bytes);
     bf3_mfma<NB>(acc, P);
     __builtin_amdgcn_sched_barrier(0);
     bf3_split<NB, USER>(P, cacc, sacc, wsum, Fr, w);
@@ -896,7 +921,7 @@ __device__ __forceinline__ void gram_wave(
 // the FUSE form, whose waves then start the CG solve on their entity
 // (start_from_acc; split entities are started after slab_reduce) and meet
 // once at the end to store the block's (r.r, p.Gp) pair.
-template <int NB, bool USER, bool FUSE>
+template <int NB, bool USER, bool FUSE, bool BUF>
 __global__ __launch_bounds__(256, (NB <= 4 ? 3 : 1)) void gram_kernel(
     const WorkItem* __restrict__ work, int64_t n_work,
     const int32_t* __restrict__ idx, const float* __restrict__ val,
@@ -907,13 +932,13 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 3 : 1)) void gram_kernel(
   double drr = 0.0, dpq = 0.0;
   if constexpr (!FUSE) {
     if (wi >= n_work) return;
-    gram_wave<NB, USER, false>(wi, work, idx, val, F, bias, k, ldk, zrow, direct, slab, cs,
-                               nullptr, drr, dpq);
+    gram_wave<NB, USER, false, BUF>(wi, work, idx, val, F, bias, k, ldk, zrow, direct, slab, cs,
+                                    nullptr, drr, dpq);
   } else {
     __shared__ StartScratch<NB> scr[GRAM_WAVES];
     if (wi < n_work)
-      gram_wave<NB, USER, true>(wi, work, idx, val, F, bias, k, ldk, zrow, direct, slab, cs,
-                                &scr[wid], drr, dpq);
+      gram_wave<NB, USER, true, BUF>(wi, work, idx, val, F, bias, k, ldk, zrow, direct, slab,
+                                     cs, &scr[wid], drr, dpq);
     store_start_pair(drr, dpq, cs.parts);
   }
 }
@@ -940,13 +965,25 @@ static int launch_gram_nb(hipStream_t s, bool user_side, int k, const WorkItem* 
   if (n_work <= 0) return 0;
   const int64_t grid = (n_work + GRAM_WAVES - 1) / GRAM_WAVES;
   const CgStart cs = start ? *start : CgStart{};
-#define MR_GRAM_LAUNCH(U, FU)                                                           \
-  MR_LAUNCH((gram_kernel<NB, U, FU>), dim3((unsigned)grid), dim3(256), 0, s, work, n_work, \
+  // buffer-resource gathers when the whole table (zrow + 1 rows) is < 2 GiB
+  // and the row segment is whole dwordx4s (NB = 4, 8)
+  constexpr bool BUFOK = NB % 4 == 0;
+  const bool buf = BUFOK && (int64_t)(zrow + 1) * ldk_of(k) * 4 < ((int64_t)1 << 31);
+#define MR_GRAM_LAUNCH(U, FU, B)                                                          \
+  MR_LAUNCH((gram_kernel<NB, U, FU, B>), dim3((unsigned)grid), dim3(256), 0, s, work, n_work, \
             idx, val, F, bias, k, ldk_of(k), zrow, direct, slab, cs)
-  if (user_side) {
-    if (start) MR_GRAM_LAUNCH(true, true); else MR_GRAM_LAUNCH(true, false);
+  if (buf) {
+    if (user_side) {
+      if (start) MR_GRAM_LAUNCH(true, true, BUFOK); else MR_GRAM_LAUNCH(true, false, BUFOK);
+    } else {
+      if (start) MR_GRAM_LAUNCH(false, true, BUFOK); else MR_GRAM_LAUNCH(false, false, BUFOK);
+    }
   } else {
-    if (start) MR_GRAM_LAUNCH(false, true); else MR_GRAM_LAUNCH(false, false);
+    if (user_side) {
+      if (start) MR_GRAM_LAUNCH(true, true, false); else MR_GRAM_LAUNCH(true, false, false);
+    } else {
+      if (start) MR_GRAM_LAUNCH(false, true, false); else MR_GRAM_LAUNCH(false, false, false);
+    }
   }
 #undef MR_GRAM_LAUNCH
   MR_HIP(hipGetLastError());
