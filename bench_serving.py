@@ -18,6 +18,9 @@ One JSON line per workload (synthetic data of the ML-full shape, seeded):
 * ``similar`` -- similar-movie lists per second (``build_similar_movies_db``:
   every movie against every movie through co-rating users, genre gate, top
   20), all 58k movies of the ML-full raw shape (23.3 M ratings).
+* ``fsim``   -- movie-movie cosine lists per second on the ALS factor layout
+  (north star; ``similar.similar_by_factors``): all 50,367 movies x k = 64,
+  top 20 other movies each, on the serving score / select kernels.
 * ``prep``   -- training ratings per second through the ALS data preparation
   (``movie_lens_data.py:547-680``): medians, the in-place shrink for the
   reference's factors (3, 5, 7, 9, 11), first-appearance id order and the
@@ -358,9 +361,56 @@ def bench_similar(a):
          {"wall_inclusive": M / wall, "movies_with_results": int((oc > 0).sum())})
 
 
+def bench_fsim(a):
+    from movie_recommender_amd.serving import MovieTable
+    k, nm, N = 64, 50_367, 20
+    V, als_ids, _, mids, _ = movie_side(k, nm, 1)
+    V = V.reshape(nm, k)
+    Vn = V / np.linalg.norm(V, axis=1)[:, None]
+    zero_med = {m: 0.0 for m in als_ids}
+    X = np.zeros((nm, k + 1))
+    X[:, :k] = Vn
+    self_excl = [[int(m)] for m in mids]
+    with MovieTable(k, Vn, als_ids, zero_med) as t:
+        t.top_n_arrays(X[:256], self_excl[:256], N)                 # warm-up
+        best = None
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            t.top_n_arrays(X, self_excl, N)
+            wall = time.perf_counter() - t0
+            ms = t.kernel_ms()
+            dev = ms["scores"] + ms["exclude"] + ms["select"]
+            if best is None or dev < best[0]:
+                best = (dev, wall, ms)
+    dev, wall, ms = best
+    flops = nm * nm * (2.0 * k + 2)
+    score_tfs = flops / (ms["scores"] * 1e-3) / 1e12
+    roof = {"kernel": "rec_score_kernel", "bound": "fp64-valu", "achieved": round(score_tfs, 2),
+            "peak": FP64_PEAK_TFS, "unit": "TFLOP/s", "frac": round(score_tfs / FP64_PEAK_TFS, 4),
+            "traffic": None, "avg_launch_ms": round(ms["scores"], 3),
+            "select_ms": round(ms["select"], 3)}
+    cpu = None
+    if not a.no_cpu:
+        ns = 200
+        t0 = time.perf_counter()
+        for j in range(ns):          # cosine of one movie against all, top 20 by (score, id)
+            sc = Vn @ Vn[j]
+            sc[j] = -np.inf
+            top = np.lexsort((-mids, -sc))[:N]
+        dt = time.perf_counter() - t0
+        cpu = {"value": ns / dt, "unit": "lists/s",
+               "cores": int(os.environ.get("OMP_NUM_THREADS", "1")), "kind": "port",
+               "sample": f"{ns} query movies: NumPy cosine against all {nm} (BLAS GEMV, "
+                         "OMP_NUM_THREADS threads) and a (score, id) sort"}
+    line("movie-movie cosine lists/s (factor layout, 50k movies, k=64, top 20)",
+         nm / (dev * 1e-3), "lists/s",
+         {"workload": "factor cosine top-N", "movies": nm, "k": k, "num_results": N},
+         roof, cpu, {"wall_inclusive": nm / wall, "kernel_ms": ms})
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--what", default="topn,eval,foldin,prep,similar")
+    ap.add_argument("--what", default="topn,eval,foldin,prep,similar,fsim")
     ap.add_argument("--users", type=int, default=65536)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true")
@@ -368,7 +418,7 @@ def main():
     for w in a.what.split(","):
         t0 = time.time()
         {"topn": bench_topn, "eval": bench_eval, "foldin": bench_foldin, "prep": bench_prep,
-         "similar": bench_similar}[w](a)
+         "similar": bench_similar, "fsim": bench_fsim}[w](a)
         log(f"[bench_serving] {w} done in {time.time() - t0:.1f}s")
 
 
