@@ -1168,8 +1168,8 @@ __global__ __launch_bounds__(256) void gram_largek_kernel(
 #pragma unroll
     for (int x = 0; x < 4; ++x) acc[j][x] = 0.0;
   }
-  // group 0, thread v < ldk: rhs / row sum of virtual column v
-  double cv = 0.0, sv = 0.0, wsum = 0.0;
+  // group 0: rhs / row sums of virtual columns tid and tid + 256 (ldk <= 512)
+  double cv[2] = {0.0, 0.0}, sv[2] = {0.0, 0.0}, wsum = 0.0;
   for (int base = 0; base < wlen; base += LK_ROWS) {
     const int n = min(LK_ROWS, wlen - base);
     __syncthreads();
@@ -1213,10 +1213,16 @@ __global__ __launch_bounds__(256) void gram_largek_kernel(
           for (int x = 0; x < 4; ++x) acc[j][x] = fma(av, (double)a[ca[j] + x], acc[j][x]);
         }
       }
-      if (group == 0 && tid < ldk) {
-        const double av = a[tid];
-        cv = fma(av, (double)wts[t], cv);
-        if (USER) sv += av;
+      if (group == 0) {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int vc = tid + 256 * hh;
+          if (vc < ldk) {
+            const double av = a[vc];
+            cv[hh] = fma(av, (double)wts[t], cv[hh]);
+            if (USER) sv[hh] += av;
+          }
+        }
       }
       if (USER) wsum += wts[t];
     }
@@ -1235,10 +1241,14 @@ __global__ __launch_bounds__(256) void gram_largek_kernel(
       Ge[(int64_t)NTILE * 256 + (t - NO) * 16 + rr] = (float)sd[j];
   }
   if (group == 0) {
-    if (tid < ldk) {
-      const int nn = NB * (tid & 15) + (tid >> 4);   // natural column of virtual tid
-      D.C[di * D.sV + nn] = nn < k ? (float)cv : 0.f;
-      if (USER) D.Gs[di * D.sV + nn] = nn < k ? (float)sv : 0.f;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int vc = tid + 256 * hh;
+      if (vc < ldk) {
+        const int nn = NB * (vc & 15) + (vc >> 4);   // natural column of virtual vc
+        D.C[di * D.sV + nn] = nn < k ? (float)cv[hh] : 0.f;
+        if (USER) D.Gs[di * D.sV + nn] = nn < k ? (float)sv[hh] : 0.f;
+      }
     }
     if (USER && tid == 0) {
       D.Cb[di * D.sS] = (float)wsum;

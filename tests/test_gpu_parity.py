@@ -228,7 +228,7 @@ def test_replay_from_snapshot_is_bitwise_identical(gpu):
         assert np.array_equal(U, U1) and np.array_equal(V, V1)
 
 
-@pytest.mark.parametrize("k", [3, 10, 16, 20, 32, 33, 64, 65, 96, 128, 144, 200])
+@pytest.mark.parametrize("k", [3, 10, 16, 20, 32, 33, 64, 65, 96, 128, 144, 200, 300])
 def test_gram_kernel_vs_numpy(gpu, k):
     """Normal equations of both sides against fp64 NumPy -- VALU fp32 for
     k < 32, bf16x3 split on the bf16 MFMA for 32 <= k <= 128, the streamed
@@ -263,7 +263,7 @@ def test_gram_kernel_vs_numpy(gpu, k):
     _lib.check(_lib.lib().mr_set_gram_chunk(2048), "reset chunk")
 
 
-@pytest.mark.parametrize("k", [5, 10, 32, 33, 64, 65, 128, 144, 200])
+@pytest.mark.parametrize("k", [5, 10, 32, 33, 64, 65, 128, 144, 200, 300])
 @pytest.mark.parametrize("fuse,chunk", [(1, 2048), (1, 64), (0, 2048)])
 def test_cg_iterations_vs_oracle(gpu, k, fuse, chunk):
     """The first CG iterations of both sides -- CG start (fused in the Gram
