@@ -18,8 +18,9 @@ items sharded by rating count (weak scaling is not available for a fixed
 data set: per-rank work shrinks as N grows -> "strong").
 
 Printed on rank 0: ONE JSON line with the contract fields plus
-``roofline`` (dominant kernel, from HIP events on the engine's stream over the
-timed region) and ``cpu_baseline`` (the reference library compiled from
+``roofline`` (dominant kernel, from HIP events on the engine's stream over an
+instrumented replay of the timed steps; the timed region itself carries no
+per-launch events) and ``cpu_baseline`` (the reference library compiled from
 /root/reference sources, oracle/_ref/cpp_ls_lib.so, timed on a bounded
 sample of the same workload; N = 1 only).
 """
@@ -245,52 +246,56 @@ def main():
         ctx.iterate(1)
     ctx.sync()
     ctx.reset_stats()
-    ctx.set_timing(not args.no_kernel_events)
 
     def barrier():
         ctx.sync()
         if dist is not None:
             dist.barrier()
 
-    # snapshot of the iterate: the event-free pass below replays the SAME
-    # steps (bit-identical kernels, so identical CG iteration counts)
-    replay = not args.no_kernel_events and n_users * (k + 1) + n_items * k < 200_000_000
-    snap = ctx.get_factors() if replay else None
-    barrier()
-    t_start = time.perf_counter()
-    for s in range(args.steps):
-        ctx.iterate(1)
-    barrier()
-    elapsed = time.perf_counter() - t_start
-    if dist is not None:
+    def max_over_ranks(x):
+        if dist is None:
+            return x
         import torch
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        tt = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local_rank}")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        return float(tt.item())
+
+    def timed_steps():
+        barrier()
+        t = time.perf_counter()
+        for s in range(args.steps):
+            ctx.iterate(1)
+        barrier()
+        return max_over_ranks(time.perf_counter() - t)
+
+    # The timed region runs WITHOUT per-launch events (the workload only);
+    # then the SAME K steps are replayed from a snapshot of the iterate with a
+    # start/stop HIP event pair on every launch (hipExtLaunchKernel, on the
+    # engine's stream) for the per-kernel table and the roofline.  The engine
+    # is deterministic, so the replay runs bit-identical kernels: its CG
+    # iteration counts must equal the timed pass's (replay_cg_identical).
+    # Tables too large to snapshot (C5) time one instrumented pass instead.
+    instrument = not args.no_kernel_events
+    replay = instrument and n_users * (k + 1) + n_items * k < 200_000_000
+    snap = ctx.get_factors() if replay else None
+    ctx.set_timing(instrument and not replay)
+    elapsed = timed_steps()
     st = ctx.stats()
-    ctx.set_timing(False)
-    # The same K steps again without per-launch events, replayed from the
-    # snapshot (informational: the event timestamps of hipExtLaunchKernel
-    # cost a few us per launch).
-    plain_ms = None
+    events_ms = None
     replay_identical = None
     if replay:
         ctx.set_factors(*snap)
         ctx.reset_stats()
-        barrier()
-        t1 = time.perf_counter()
-        for s in range(args.steps):
-            ctx.iterate(1)
-        barrier()
-        plain_ms = (time.perf_counter() - t1) * 1e3 / args.steps
-        st2 = ctx.stats()
-        replay_identical = (st2["cg_users_total"] == st["cg_users_total"]
-                            and st2["cg_items_total"] == st["cg_items_total"])
-        if dist is not None:
-            import torch
-            tt = torch.tensor([plain_ms], dtype=torch.float64, device=f"cuda:{local_rank}")
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            plain_ms = float(tt.item())
+        ctx.set_timing(True)
+        events_ms = timed_steps() * 1e3 / args.steps
+        st_ev = ctx.stats()
+        replay_identical = (st_ev["cg_users_total"] == st["cg_users_total"]
+                            and st_ev["cg_items_total"] == st["cg_items_total"])
+        for key in ("kernel_ms", "kernel_launches", "phase_ms"):
+            st[key] = st_ev[key]
+    elif instrument:
+        events_ms = elapsed * 1e3 / args.steps
+    ctx.set_timing(False)
 
     # local work units (ratings processed by this rank per iteration)
     n_local_users = ctx.num_ratings
@@ -371,7 +376,11 @@ def main():
                           "per_step_items": st["cg_items_total"] / args.steps},
         "kernels": kernel_table,
         "phase_ms_per_step": {p: round(v / args.steps, 3) for p, v in st["phase_ms"].items()},
-        "ms_per_step_without_kernel_events": round(plain_ms, 3) if plain_ms else None,
+        "timing": ("timed region without per-launch events; kernel table and roofline from "
+                   "an event-instrumented replay of the same steps" if replay else
+                   "one event-instrumented timed region" if instrument else
+                   "timed region without per-launch events (no kernel table)"),
+        "ms_per_step_with_kernel_events": round(events_ms, 3) if events_ms else None,
         "replay_cg_identical": replay_identical,
     }
     if rank == 0 and world == 1 and not args.no_cpu and not c5:

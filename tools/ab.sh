@@ -12,5 +12,5 @@ for v in $ORDER; do
   rc=$?; if [ $rc -ne 0 ]; then echo "$v rc=$rc: stop"; tail -5 $OUT/${n}_$v.err; exit $rc; fi
   python3 -c "
 import json,sys; d=json.load(open('$OUT/${n}_$v.json'))
-k=d['kernels']; print('$v', round(d['value']/1e9,3), d['ms_per_step'], d['ms_per_step_without_kernel_events'], d['cg_iterations']['users_total'], d['cg_iterations']['items_total'], ' '.join(f'{c}={v[\"avg_us\"]}' for c,v in k.items()))"
+k=d['kernels']; print('$v', round(d['value']/1e9,3), d['ms_per_step'], d['ms_per_step_with_kernel_events'], d['cg_iterations']['users_total'], d['cg_iterations']['items_total'], ' '.join(f'{c}={v[\"avg_us\"]}' for c,v in k.items()))"
 done
