@@ -164,7 +164,13 @@ __device__ __forceinline__ void tile_matvec(
   const int lane = threadIdx.x & 63;
   const int rr = lane >> 2, c4 = (lane & 3) * 4;
   auto tile = [&](int t, double (&ge)[4]) {
-    const float4 gg = g[t];
+    float4 gg = g[t];
+    // NB > 4: an opaque copy, so the two passes convert each tile afresh
+    // instead of keeping every tile's fp64 copy live between them (GVN would
+    // merge the conversions: 352 -> 256 VGPRs, 2 waves/SIMD at k = 128; the
+    // values are the same, so the results are bit-identical).  At NB <= 4 the
+    // merged form fits 4 waves/SIMD and measured faster.
+    if constexpr (NB > 4) asm volatile("" : "+v"(gg.x), "+v"(gg.y), "+v"(gg.z), "+v"(gg.w));
     ge[0] = gg.x; ge[1] = gg.y; ge[2] = gg.z; ge[3] = gg.w;
   };
   // diagonal tile of block b and whether its stored triangle is the lower one
@@ -1619,7 +1625,7 @@ __device__ void last_block_finalize(CgState* st, int phase, double* partials, Cg
 // users 225 -> 195 us, items 103 -> 94 us, and the CG update 28 -> 25 us
 // because its vectors stay cached).
 template <int NB, bool USER>
-__global__ __launch_bounds__(256, (NB <= 4 ? 4 : 1)) void cg_matvec_kernel(
+__global__ __launch_bounds__(256, (NB <= 4 ? 4 : 2)) void cg_matvec_kernel(
     const CgState* __restrict__ st, int update_p, int64_t E, int k, int ldk,
     const float* __restrict__ G, const float* __restrict__ Gs,
     const float* __restrict__ Gn, double* __restrict__ v, double* __restrict__ vb,
