@@ -332,7 +332,10 @@ def main():
     if os.path.exists(args.pmc):
         with open(args.pmc) as f:
             pmc = json.load(f)
-        traffic = pmc.get("hbm_bytes_per_launch", {}).get(cls)
+        # only for the workload the counter passes ran (per-launch bytes)
+        wl = pmc.get("workload", {"shape": "ml-full", "k": 64})
+        if wl.get("shape") == args.shape and wl.get("k") == k and world == 1 and not c5:
+            traffic = pmc.get("hbm_bytes_per_launch", {}).get(cls)
     kernel_table = {}
     for c, ms in st["kernel_ms"].items():
         n = st["kernel_launches"][c]
@@ -363,7 +366,8 @@ def main():
                                 + f", k={k}, solver={args.solver}"),
                    "k": k, "n_ratings": int(n_total), "users": int(n_users),
                    "items": int(n_items), "solver": args.solver,
-                   "parallelism": f"shard{world}" if world > 1 else "single"},
+                   "parallelism": (f"shard{world}" if world > 1 or args.force_shard
+                                   else "single")},
         "roofline": {"kernel": cls, "bound": bound, "achieved": round(achieved, 2),
                      "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
                      "traffic": traffic,

@@ -60,11 +60,14 @@ def main():
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--shape", default="ml-full", help="bench workload the passes ran")
+    ap.add_argument("--k", type=int, default=64)
     a = ap.parse_args()
     fe = read_counter(a.fetch, "FETCH_SIZE")
     wr = read_counter(a.write, "WRITE_SIZE")
     res = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
                      "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 per active dispatch",
+           "workload": {"shape": a.shape, "k": a.k},
            "per_kernel": {}, "hbm_bytes_per_launch": {}}
     for cls in sorted(set(fe) | set(wr)):
         f = fe.get(cls, {}).get("mean_kb", 0.0)
