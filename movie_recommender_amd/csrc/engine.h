@@ -102,6 +102,7 @@ struct Engine {
            const int* uv_iid, const double* uv_r, int64_t n_i, const int* iv_uid,
            const int* iv_iid, const double* iv_r, int64_t u0, int64_t u1, int64_t i0,
            int64_t i1);
+  int place_chunks_by_xcd(Side& S, std::vector<WorkItem>& work, int64_t chunk);
   int build_side(Side& S, bool user, int64_t n, const int32_t* d_key,
                  const int32_t* d_other, const double* d_r);
   int set_factors(const double* hU, const double* hV);

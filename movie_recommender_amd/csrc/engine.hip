@@ -166,6 +166,61 @@ int Engine::resolve_timing() {
 // ----------------------------------------------------------------------------
 // construction
 // ----------------------------------------------------------------------------
+// XCD-aware placement of the heavy entities' chunks in the Gram work list.
+// Gram block b holds work items 4b .. 4b+3 and blocks are dealt round-robin
+// over the 8 XCDs (MI355X_MICROARCH.md), so the XCD of list position p is
+// (p / 4) mod 8.  A heavy entity's rating list is cut into full chunks of
+// `chunk` ratings; within an entity the ratings are ordered by opposite id
+// (the CSR build sorts stably, and the data arrive grouped by user), so a
+// chunk gathers opposite rows from a narrow id range.  The full chunks are
+// dealt to the chunk positions so that XCD x receives the x-th eighth of them
+// in opposite-id order (key = the id at the chunk's middle): each XCD's L2
+// then serves ~1/8 of the opposite table for this share of the gathers.
+// Bit-identical: every chunk keeps its ratings and its slab record (summed by
+// slab_reduce in chunk order), unsplit entities keep their positions (the
+// fused CG start's per-block partial sums), and chunk waves add nothing to
+// those sums -- only which CU runs which chunk changes.  Applied to the
+// matrix-core Gram (32 <= k <= 128, four work items per block) when the
+// opposite table exceeds 16 MiB (four XCDs' L2): ML-full k = 64 items side
+// (U, 26 MB) 606 -> 582 us same-box; the users side (V, 13 MB, ~60 % L2
+// hits already) measured no gain.
+int Engine::place_chunks_by_xcd(Side& S, std::vector<WorkItem>& work, int64_t chunk) {
+  constexpr int64_t kWaves = 4, kXcds = 8;
+  const int64_t table = (S.user ? I : U) * (int64_t)ldk * 4;
+  if (k < 32 || k > 128 || table <= ((int64_t)16 << 20)) return 0;
+  std::vector<int64_t> pos;
+  for (int64_t p = 0; p < (int64_t)work.size(); ++p)
+    if (work[p].slab >= 0 && work[p].len == chunk) pos.push_back(p);
+  const int64_t nc = (int64_t)pos.size();
+  if (nc < 2 * kWaves * kXcds) return 0;
+  std::vector<int64_t> mid(nc);
+  for (int64_t j = 0; j < nc; ++j) mid[j] = work[pos[j]].begin + work[pos[j]].len / 2;
+  int64_t* d_mid = nullptr;
+  int32_t* d_key = nullptr;
+  if (dalloc(&d_mid, nc, stream) || dalloc(&d_key, nc, stream)) return -1;
+  std::vector<int32_t> key(nc);
+  int rc = 0;
+  do {
+    if (t_stager.h2d(stream, d_mid, mid.data(), (size_t)nc * sizeof(int64_t))) { rc = -1; break; }
+    if (launch_gather_i32(stream, nc, d_mid, S.idx, d_key)) { rc = -1; break; }
+    if (t_stager.d2h(stream, key.data(), d_key, (size_t)nc * sizeof(int32_t))) { rc = -1; break; }
+  } while (0);
+  dfree(d_mid, stream);
+  dfree(d_key, stream);
+  if (rc) return rc;
+  std::vector<int64_t> by_key(nc), slots(pos);
+  for (int64_t j = 0; j < nc; ++j) by_key[j] = j;
+  std::stable_sort(by_key.begin(), by_key.end(),
+                   [&](int64_t a, int64_t b) { return key[a] < key[b]; });
+  std::stable_sort(slots.begin(), slots.end(), [&](int64_t a, int64_t b) {
+    return (a / kWaves) % kXcds < (b / kWaves) % kXcds;
+  });
+  std::vector<WorkItem> chunks(nc);
+  for (int64_t j = 0; j < nc; ++j) chunks[j] = work[pos[by_key[j]]];
+  for (int64_t j = 0; j < nc; ++j) work[slots[j]] = chunks[j];
+  return 0;
+}
+
 int Engine::build_side(Side& S, bool user, int64_t n, const int32_t* d_key,
                        const int32_t* d_other, const double* d_r) {
   S.user = user;
@@ -202,6 +257,7 @@ int Engine::build_side(Side& S, bool user, int64_t n, const int32_t* d_key,
   }
   std::stable_sort(work.begin(), work.end(),
                    [](const WorkItem& a, const WorkItem& b) { return a.len > b.len; });
+  if (place_chunks_by_xcd(S, work, chunk)) return -1;
   S.n_work = (int64_t)work.size();
   S.n_split = (int64_t)split.size();
   S.n_slab = nslab;

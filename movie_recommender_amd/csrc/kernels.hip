@@ -2478,6 +2478,20 @@ int launch_rows_of(hipStream_t s, int64_t rows, const int64_t* rp, int32_t* row_
   return 0;
 }
 
+__global__ void gather_i32_kernel(int64_t n, const int64_t* __restrict__ pos,
+                                  const int32_t* __restrict__ src, int32_t* __restrict__ dst) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n;
+       t += (int64_t)gridDim.x * blockDim.x)
+    dst[t] = src[pos[t]];
+}
+int launch_gather_i32(hipStream_t s, int64_t n, const int64_t* pos, const int32_t* src,
+                      int32_t* dst) {
+  if (n <= 0) return 0;
+  gather_i32_kernel<<<grid_for(n), 256, 0, s>>>(n, pos, src, dst);
+  MR_HIP(hipGetLastError());
+  return 0;
+}
+
 __global__ void i32_to_i64_kernel(int64_t n, const int32_t* __restrict__ in,
                                   int64_t* __restrict__ out) {
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n;

@@ -293,6 +293,9 @@ int launch_p_update_f64(hipStream_t s, const CgState* st, int64_t n,
 int launch_rows_of(hipStream_t s, int64_t rows, const int64_t* rp,
                    int32_t* row_of);
 int launch_i32_to_i64(hipStream_t s, int64_t n, const int32_t* in, int64_t* out);
+// dst[t] = src[pos[t]] (t < n)
+int launch_gather_i32(hipStream_t s, int64_t n, const int64_t* pos, const int32_t* src,
+                      int32_t* dst);
 int launch_validate_ids(hipStream_t s, int64_t n, const int32_t* ids, int32_t lo,
                         int32_t hi, int* bad);
 

@@ -495,10 +495,14 @@ def test_full_size_gram_sampled(gpu):
         assert its >= 1 and np.isfinite(rr)
 
 
-def expected_layout(ids, other, ratings, E, chunk=2048):
+def expected_layout(ids, other, ratings, E, chunk=2048, xcd_table_bytes=0):
     """Host restatement of the context build: stable CSR by entity, then the
     Gram work list (entities longer than `chunk` split into slabs numbered in
-    entity order; stable sort by length, heavy first) -- engine.hip build_side."""
+    entity order; stable sort by length, heavy first) -- engine.hip build_side
+    -- and, when the opposite table exceeds 16 MiB, the XCD placement of the
+    full chunks (engine.hip place_chunks_by_xcd: chunks in order of the
+    opposite id at their middle, dealt to the chunk positions grouped by XCD
+    = (position // 4) % 8)."""
     order = np.argsort(ids, kind="stable")
     off = np.zeros(E + 1, np.int64)
     np.cumsum(np.bincount(ids, minlength=E), out=off[1:])
@@ -515,7 +519,16 @@ def expected_layout(ids, other, ratings, E, chunk=2048):
                 work.append((b, min(chunk, int(off[e + 1]) - b), e, nslab + c))
             nslab += nc
     work.sort(key=lambda w: -w[1])     # stable: equal lengths keep entity order
-    return off, other[order].astype(np.int32), ratings[order].astype(np.float32), work
+    cidx = other[order].astype(np.int32)
+    pos = [p for p, w in enumerate(work) if w[3] >= 0 and w[1] == chunk]
+    if xcd_table_bytes > (16 << 20) and len(pos) >= 64:
+        key = [int(cidx[work[p][0] + work[p][1] // 2]) for p in pos]
+        by_key = sorted(range(len(pos)), key=lambda j: key[j])
+        slots = sorted(pos, key=lambda p: (p // 4) % 8)
+        chunks = [work[pos[j]] for j in by_key]
+        for j, sl in enumerate(slots):
+            work[sl] = chunks[j]
+    return off, cidx, ratings[order].astype(np.float32), work
 
 
 def test_full_size_context_build_exact(gpu):
@@ -532,7 +545,9 @@ def test_full_size_context_build_exact(gpu):
             ids, other, E = ((rs.user_ids, rs.item_ids, rs.num_users) if side == "users"
                              else (rs.item_ids, rs.user_ids, rs.num_items))
             off, idx, val, (wb, wl, we, ws) = ctx.layout(side)
-            eoff, eidx, eval_, work = expected_layout(ids, other, rs.ratings, E)
+            n_other = rs.num_items if side == "users" else rs.num_users
+            eoff, eidx, eval_, work = expected_layout(ids, other, rs.ratings, E,
+                                                      xcd_table_bytes=n_other * 64 * 4)
             assert np.array_equal(off, eoff), side
             assert np.array_equal(idx, eidx), side
             assert np.array_equal(val, eval_), side
