@@ -744,9 +744,23 @@ __device__ __forceinline__ void bf3_mfma(floatx4 (&acc)[NB * (NB + 1) / 2],
     for (int bi = 0; bi < NB; ++bi)
 #pragma unroll
       for (int bj = bi; bj < NB; ++bj) {
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-            __builtin_bit_cast(bf16x8_t, P[pa][bi]), __builtin_bit_cast(bf16x8_t, P[pb][bj]),
-            acc[t], 0, 0, 0);
+        if constexpr (NB >= 5) {
+          // the same instruction with the accumulator pinned to AGPRs: with
+          // the builtin, the allocator kept part of the NB >= 5 accumulators
+          // in VGPRs inside the loop and copied them to / from AGPRs every
+          // half (200 v_accvgpr_* per half at NB = 8; loop 984 -> 783
+          // instructions; k = 128 Gram users 1313 -> 1255 us, items 1001 ->
+          // 960 us same-box, bit-identical).  The hazard windows are covered
+          // by the code around the loop: the split's ~500 VALU separate the
+          // last MFMA from the epilogue's accumulator reads, and the gathers
+          // separate the split's P writes from the next MFMAs.
+          asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+              : "+a"(acc[t]) : "v"(P[pa][bi]), "v"(P[pb][bj]));
+        } else {
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8_t, P[pa][bi]), __builtin_bit_cast(bf16x8_t, P[pb][bj]),
+              acc[t], 0, 0, 0);
+        }
         ++t;
       }
   }
