@@ -93,25 +93,37 @@ __global__ __launch_bounds__(256) void rec_score_kernel(
   for (int p = 0; p < 8; ++p)
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[p][q] = 0.0;
-  // staging: thread owns factor column jj = tid & 15 of rows (tid >> 4) + 16 i
+  // staging: thread owns factor column jj = tid & 15 of rows (tid >> 4) + 16 i.
+  // The next k-chunk is loaded into registers while this one is multiplied
+  // (one chunk ahead), so the L2 / MALL latency of the staging loads overlaps
+  // the arithmetic; LDS holds only the current chunk.
   const int jj = tid & 15, rr = tid >> 4;
-  for (int j0 = 0; j0 < k; j0 += SC_KC) {
+  static_assert(SC_U * SC_KC / 2 == 256, "one x pair per thread");
+  double vreg[SC_C / 16], xreg[2];
+  auto load_chunk = [&](int j0) {
     const int kc = min(SC_KC, k - j0);
     const bool jok = jj < kc;
     const double* src = Vc + (int64_t)(c0 + rr) * k + j0 + jj;
-#pragma unroll 4
+#pragma unroll
     for (int i = 0; i < SC_C / 16; ++i) {
       const bool ok = jok && (c0 + rr + 16 * i) < n_cand;
-      vs[rr + 16 * i][jj] = ok ? src[(int64_t)16 * i * k] : 0.0;
+      vreg[i] = ok ? src[(int64_t)16 * i * k] : 0.0;
     }
-    if (tid < SC_U * SC_KC / 2) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int r = rr + 16 * i, u = u0 + r;
-        xs[r][jj] = (jok && u < n_users) ? X[(int64_t)u * (k + 1) + j0 + jj] : 0.0;
-      }
+    for (int i = 0; i < 2; ++i) {
+      const int r = rr + 16 * i, u = u0 + r;
+      xreg[i] = (jok && u < n_users) ? X[(int64_t)u * (k + 1) + j0 + jj] : 0.0;
     }
+  };
+  load_chunk(0);
+  for (int j0 = 0; j0 < k; j0 += SC_KC) {
+    const int kc = min(SC_KC, k - j0);
+#pragma unroll
+    for (int i = 0; i < SC_C / 16; ++i) vs[rr + 16 * i][jj] = vreg[i];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) xs[rr + 16 * i][jj] = xreg[i];
     __syncthreads();
+    if (j0 + SC_KC < k) load_chunk(j0 + SC_KC);
     for (int j = 0; j < kc; ++j) {
       double xv[8], vv[4];
 #pragma unroll
