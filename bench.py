@@ -62,7 +62,7 @@ def load_data(shape, k, cache_dir="/tmp"):
     return rs
 
 
-def algorithmic_cost(cls, k, n_users, n_items, n_ratings, ldk, fused=True):
+def algorithmic_cost(cls, k, n_users, n_items, n_ratings, ldk, fused=True, n_ratings_items=None):
     """(bytes, flops) per launch of a kernel class; definitions in DESIGN.md.
 
     Normal equations are stored "tri16" (mr_internal.h): the nb(nb-1)/2
@@ -80,6 +80,7 @@ def algorithmic_cost(cls, k, n_users, n_items, n_ratings, ldk, fused=True):
     K = k + 1
     nb = (k + 15) // 16
     gsz = (nb * (nb - 1) // 2 + nb // 2 + nb % 2) * 256 + (nb // 2) * 16
+    n_ri = n_ratings if n_ratings_items is None else n_ratings_items   # item-view ratings
     if cls == "matvec_users":
         E = n_users
         g = E * (gsz + ldk + 1) * 4               # G_e blocks + Gs row + count
@@ -95,10 +96,10 @@ def algorithmic_cost(cls, k, n_users, n_items, n_ratings, ldk, fused=True):
             b += n_users * (ldk + 1) * (4 + 3 * 8)
         return b, n_ratings * (1.0 * K * (K + 1) + 2.0 * K)
     if cls == "gram_items":
-        b = n_ratings * (8 + 4 * (k + 1)) + n_items * (gsz + ldk) * 4
+        b = n_ri * (8 + 4 * (k + 1)) + n_items * (gsz + ldk) * 4
         if fused:
             b += n_items * ldk * (4 + 3 * 8)
-        return b, n_ratings * (1.0 * k * (k + 1) + 2.0 * k)
+        return b, n_ri * (1.0 * k * (k + 1) + 2.0 * k)
     if cls == "cg_update":
         # x rw (fp32), r rw, p read, q read (fp64)
         E = (n_users * (ldk + 1) + n_items * ldk) / 2.0   # average side
@@ -118,17 +119,53 @@ def iteration_roofline(k, rate):
             "fp32_TFps": round(F * rate / 1e12, 2), "fp32_frac": round(F * rate / 157.3e12, 4)}
 
 
-def cpu_baseline(shape, k, threads, scale, seed=0):
+def cpu_share():
+    """CPUs this process may use: the scheduler affinity mask, capped by the
+    cgroup CPU quota (cgroup v2 cpu.max / v1 cfs quota) -- on the GPU box
+    ``nproc`` shows the whole machine while the job gets a share of it."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = int(f.read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    n = aff if quota is None else max(1, min(aff, int(quota)))
+    return n, {"host_cpus": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota}
+
+
+def cpu_baseline(shape, k, threads, scale, seed=0, replay=True):
     """Reference CPU path on a bounded sample of the same workload: the
     MovieLens-shaped generator at ``scale`` of the users, items and draws (so
     per-entity degrees, and with them the CPU's per-rating costs, keep their
     full-size distribution; a user subsample would keep every item and with
     it the reference's full-length per-thread SpMV^T scratch), shrunk for the
-    same k.  t_iter = (T(3) - T(1)) / 2 as in BASELINE.md.  Returns a dict for
-    the JSON line, or None if the reference build is unavailable."""
+    same k.  t_iter = (T(3) - T(1)) / 2 as in BASELINE.md.  ``threads`` None:
+    the process's CPU share (``cpu_share``).
+
+    The reference's ``als()`` does not report its CG iteration counts, which
+    set its cost, so the same 3 iterations are then replayed with
+    ``oracle/ref_replay.als_replay`` -- the outer loop restated around the
+    reference's own CG, bit-identical to ``als()`` (same factors, same CG
+    trajectory) -- for the CG iterations of iterations 2-3 (the ones T(3) -
+    T(1) times) and the reference's time per CG iteration.  Returns a dict
+    for the JSON line, or None if the reference build is unavailable."""
     from oracle import ref
     if not ref.available():
         return None
+    share, cpu_info = cpu_share()
+    if threads is None:
+        threads = share
     rs = synth.movielens_like(shape, k, scale=scale)
     U0, V0 = ref.init_factors(rs.num_users, rs.num_items, k, seed)
     ref.set_thread_count(threads)
@@ -138,14 +175,48 @@ def cpu_baseline(shape, k, threads, scale, seed=0):
         ref.als(rs.user_ids, rs.item_ids, rs.ratings, k, U0, V0, max_iteration=n_it)
         t[n_it] = time.perf_counter() - t0
     t_iter = (t[3] - t[1]) / 2.0
-    return {"value": rs.n / t_iter, "unit": "ratings/s", "cores": threads,
-            "host_cpus": os.cpu_count(),
-            "kind": "reference",
-            "sample": (f"{shape} generator at scale {scale} (users, items, draws), shrunk for "
-                       f"k={k}: N={rs.n}, users={rs.num_users}, items={rs.num_items}; "
-                       f"t_iter=(T(3)-T(1))/2 = {t_iter:.3f} s (T1={t[1]:.2f} s, "
-                       f"T3={t[3]:.2f} s); oracle/_ref/cpp_ls_lib.so built from "
-                       f"/root/reference/cpp/ls_lib -O2, {threads} threads")}
+    out = {"value": rs.n / t_iter, "unit": "ratings/s", "cores": threads, **cpu_info,
+           "kind": "reference",
+           "sample": (f"{shape} generator at scale {scale} (users, items, draws), shrunk for "
+                      f"k={k}: N={rs.n}, users={rs.num_users}, items={rs.num_items}; "
+                      f"t_iter=(T(3)-T(1))/2 = {t_iter:.3f} s (T1={t[1]:.2f} s, "
+                      f"T3={t[3]:.2f} s); oracle/_ref/cpp_ls_lib.so built from "
+                      f"/root/reference/cpp/ls_lib -O2, {threads} threads")}
+    if replay:
+        from oracle.ref_replay import als_replay
+        _, _, _, tr = als_replay(rs.user_ids, rs.item_ids, rs.ratings, k, U0, V0,
+                                 max_iteration=3)
+        tr = tr[1:3]          # iterations 2-3: what T(3) - T(1) measures
+        cu = sum(x["cg_users"] for x in tr)
+        ci = sum(x["cg_items"] for x in tr)
+        tu = sum(x["t_users"] for x in tr)
+        ti = sum(x["t_items"] for x in tr)
+        out["cg"] = {
+            "per_als_iteration_users": cu / len(tr), "per_als_iteration_items": ci / len(tr),
+            "ms_per_cg_iteration_users": round(tu / max(cu, 1) * 1e3, 3),
+            "ms_per_cg_iteration_items": round(ti / max(ci, 1) * 1e3, 3),
+            # ratings x CG iterations per second: the trajectory-free rate
+            "ratings_cg_iterations_per_s": round(rs.n * (cu + ci) / (tu + ti), 1),
+            "how": ("oracle/ref_replay.als_replay: als() restated around the reference's own "
+                    "cg_least_squares_from_python, bit-identical to als_from_python "
+                    "(tests/test_oracle.py), iterations 2-3 of the same run")}
+    ref.set_thread_count(1)
+    return out
+
+
+def gpu_cg_rate(st, n_u, n_i):
+    """Time per CG iteration of each side (the solve phase's HIP-event span /
+    its CG iterations, incl. the fused start's control) and ratings x CG
+    iterations per second -- the trajectory-free rate comparable with
+    cpu_baseline.cg (the CG counts of two runs on different data differ)."""
+    cu, ci = st["cg_users_total"], st["cg_items_total"]
+    su, si = st["phase_ms"]["solve_users"], st["phase_ms"]["solve_items"]
+    if not (cu and ci and su and si):
+        return None
+    return {"ms_per_cg_iteration_users": round(su / cu, 4),
+            "ms_per_cg_iteration_items": round(si / ci, 4),
+            "ratings_cg_iterations_per_s": round((n_u * cu + n_i * ci) / ((su + si) / 1e3), 1),
+            "note": "solve phases of the instrumented replay; the Gram is not included"}
 
 
 def main():
@@ -166,7 +237,8 @@ def main():
     ap.add_argument("--cg-speculate", type=int, default=None,
                     help="engine launch-ahead level (include/mr_als.h MR_OPT_CG_SPECULATE)")
     ap.add_argument("--cpu-scale", type=float, default=0.25)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="reference threads (default: this process's CPU share)")
     ap.add_argument("--force-shard", action="store_true",
                     help="use the sharded RCCL path even with one rank (testing)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r02.json"),
@@ -303,7 +375,8 @@ def main():
     value = total_ratings * args.steps / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
 
-    # dominant kernel and its roofline (rank 0's kernels)
+    # dominant kernel and its roofline (rank 0's kernels, rank 0's shard sizes:
+    # cost-balanced shards are unequal)
     ldk = (k + 15) // 16 * 16
     if args.no_kernel_events:
         st["kernel_ms"] = {"none": 1.0}
@@ -312,9 +385,10 @@ def main():
     cls, tot_ms = best
     launches = max(1, st["kernel_launches"][cls])
     avg_s = tot_ms / launches / 1e3
-    nU = n_users // world if world > 1 else n_users
-    nI = n_items // world if world > 1 else n_items
-    nbytes, nflops = algorithmic_cost(cls, k, nU, nI, n_local_users, ldk, not args.no_fuse_start)
+    _, nU, _ = ctx.local_size("users")
+    _, nI, n_local_items = ctx.local_size("items")
+    nbytes, nflops = algorithmic_cost(cls, k, nU, nI, n_local_users, ldk, not args.no_fuse_start,
+                                      n_local_items)
     bound = "mfma" if cls.startswith("gram") and k >= 32 else "hbm"
     if bound == "hbm":
         achieved, peak, unit = nbytes / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
@@ -325,7 +399,7 @@ def main():
     # guide's measured random-row gather rate from a 38 MB table.
     gather = None
     if cls.startswith("gram"):
-        gb = n_local_users * 4.0 * k
+        gb = (n_local_users if cls == "gram_users" else n_local_items) * 4.0 * k
         gather = {"bytes_per_launch": int(gb), "achieved_GBps": round(gb / avg_s / 1e9, 1),
                   "peak_GBps": GATHER_PEAK_GBS, "frac": round(gb / avg_s / 1e9 / GATHER_PEAK_GBS, 3)}
     traffic = None
@@ -340,7 +414,8 @@ def main():
     for c, ms in st["kernel_ms"].items():
         n = st["kernel_launches"][c]
         if n:
-            b, fl = algorithmic_cost(c, k, nU, nI, n_local_users, ldk, not args.no_fuse_start)
+            b, fl = algorithmic_cost(c, k, nU, nI, n_local_users, ldk, not args.no_fuse_start,
+                                     n_local_items)
             kernel_table[c] = {"total_ms": round(ms, 3), "launches": n,
                                "avg_us": round(ms / n * 1e3, 2),
                                "alg_GBps": round(b / (ms / n / 1e3) / 1e9, 1) if b else None,
@@ -378,6 +453,7 @@ def main():
                           "items_total": st["cg_items_total"],
                           "per_step_users": st["cg_users_total"] / args.steps,
                           "per_step_items": st["cg_items_total"] / args.steps},
+        "cg_rate": gpu_cg_rate(st, n_local_users, n_local_items),
         "kernels": kernel_table,
         "phase_ms_per_step": {p: round(v / args.steps, 3) for p, v in st["phase_ms"].items()},
         "timing": ("timed region without per-launch events; kernel table and roofline from "

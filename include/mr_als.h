@@ -19,9 +19,10 @@
  *
  * Sharding (multi-GPU, one process per GPU): a context may own a contiguous
  * range of users and of items (mr_als_create_shard); factor tables stay
- * replicated, and the caller exchanges the freshly solved shard between
- * half-steps (all-gather) and the two CG scalars per CG iteration
- * (all-reduce) through the mr_comm callbacks.
+ * replicated, and the freshly solved shard is exchanged between half-steps
+ * (all-gather of equal, padded shards) and the two CG scalars per CG
+ * iteration all-reduced -- natively over RCCL (mr_als_set_rccl) or through
+ * the mr_comm callbacks.
  */
 #ifndef MR_ALS_H
 #define MR_ALS_H
@@ -70,6 +71,9 @@ typedef struct mr_stats {
  *                                     in-place all-gather of a row table:
  *                                     rank r owns rows [row_begin[r],
  *                                     row_begin[r+1]) of width row_floats
+ *                                     (the engine passes its padded
+ *                                     exchange buffer: equal blocks of
+ *                                     maxrows rows, row_begin[r] = r maxrows)
  * Both return 0 on success. */
 typedef struct mr_comm {
   void* user;
@@ -124,11 +128,13 @@ int mr_als_init_factors(mr_als* ctx, unsigned long long seed);
 int mr_als_set_solver(mr_als* ctx, int solver, double ridge);
 /* Timing of every kernel launch with HIP events (off by default). */
 int mr_als_set_timing(mr_als* ctx, int enable);
-/* Engine options (mr_als_set_option):
+/* Engine options (mr_als_set_option; in a sharded run every rank must set
+ * the same values -- they decide which launches and collectives are issued):
  *   MR_OPT_FUSE_START     1 (default): the Gram kernel also starts the CG solve
  *                         (r0, p0, q0 = G p0 from its accumulators); 0: the
  *                         reference's order, one matvec + update pass
- *   MR_OPT_CG_SPECULATE   1 (default): enqueue CG iteration t+1 before t's
+ *   MR_OPT_CG_SPECULATE   0, 1 or 2 (others are rejected).
+ *                         1 (default): enqueue CG iteration t+1 before t's
  *                         state is read back when t provably cannot stop
  *                         (decided on exact per-iteration states: identical
  *                         launches on every rank); 0: one iteration ahead;
@@ -175,6 +181,10 @@ int mr_als_get_cg_vectors(mr_als* ctx, int side, double* r, double* p, double* q
  * rating range [begin, begin+len) of local entity `entity`, slab >= 0 for a
  * chunk of a split entity).  Any pointer may be NULL.  Tests. */
 long long mr_als_work_items(mr_als* ctx, int side);
+/* This context's entities of `side`: the first global id, how many (a shard
+ * owns a contiguous range) and the ratings its CSR holds.  Any may be NULL. */
+int mr_als_local_size(mr_als* ctx, int side, long long* first, long long* count,
+                      long long* nnz);
 int mr_als_get_layout(mr_als* ctx, int side, long long* off, int* idx, float* val,
                       long long* wbegin, int* wlen, int* went, int* wslab);
 
@@ -196,6 +206,20 @@ int mr_als_device_tables(mr_als* ctx, float** Ufac, float** Ubias,
 /* Predictions u[:k].v + u[k] for n (user,item) pairs, on the device. */
 int mr_als_predict(mr_als* ctx, long long n, const int* user_ids,
                    const int* item_ids, double* out);
+
+/* Test hooks: the sharded all-gather staging kernels on host arrays (the
+ * engine runs them on its padded exchange buffers, Engine::allgather_side).
+ *   pack:    send[n*ldk] = fac rows [r0, r0+n) of a rows x ldk table
+ *            (+ send_b[n] = bias[r0 ..]; bias may be NULL)
+ *   unstage: for every rank s != skip, rows j < rb[s+1]-rb[s] of block s of
+ *            recv (world x maxrows x ldk) go to fac row rb[s]+j (+ bias from
+ *            recv_b[s*maxrows + j]); fac / bias (rb[world] rows) are in/out.
+ * ldk must be a multiple of 4; shapes are checked on the host first. */
+int mr_test_pack_rows(int device, long long rows, int ldk, const float* fac, const float* bias,
+                      long long r0, long long n, float* send, float* send_b);
+int mr_test_unstage_rows(int device, int world, int skip, const long long* rb, long long maxrows,
+                         int ldk, const float* recv, const float* recv_b, float* fac,
+                         float* bias);
 
 const char* mr_last_error(void);
 int mr_device_count(void);

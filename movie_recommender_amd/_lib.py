@@ -106,6 +106,7 @@ SIGNATURES = {
     "mr_als_iterate": (ctypes.c_int, [VP, ctypes.c_int]),
     "mr_als_half_step": (ctypes.c_int, [VP, ctypes.c_int, DP]),
     "mr_als_work_items": (ctypes.c_longlong, [VP, ctypes.c_int]),
+    "mr_als_local_size": (ctypes.c_int, [VP, ctypes.c_int, LLP, LLP, LLP]),
     "mr_als_get_layout": (ctypes.c_int, [VP, ctypes.c_int, LLP, IP, FP, LLP, IP, IP, IP]),
     "mr_als_init_factors": (ctypes.c_int, [VP, ctypes.c_ulonglong]),
     "mr_als_get_cg_vectors": (ctypes.c_int, [VP, ctypes.c_int, DP, DP, DP]),
@@ -120,6 +121,10 @@ SIGNATURES = {
     "mr_als_device_tables": (ctypes.c_int, [VP, ctypes.POINTER(FP), ctypes.POINTER(FP),
                                             ctypes.POINTER(FP), IP]),
     "mr_als_predict": (ctypes.c_int, [VP, ctypes.c_longlong, IP, IP, DP]),
+    "mr_test_pack_rows": (ctypes.c_int, [ctypes.c_int, ctypes.c_longlong, ctypes.c_int, FP, FP,
+                                         ctypes.c_longlong, ctypes.c_longlong, FP, FP]),
+    "mr_test_unstage_rows": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, LLP,
+                                            ctypes.c_longlong, ctypes.c_int, FP, FP, FP, FP]),
     # factor consumers (include/mr_serving.h)
     "mr_rec_create": (VP, [ctypes.c_int, ctypes.c_int, ctypes.c_int, DP, ctypes.c_int, IP, IP,
                            DP]),

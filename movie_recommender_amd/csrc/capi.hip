@@ -40,6 +40,22 @@ int guarded(F&& f) {
   }
   return -1;
 }
+// Device scratch of the test hooks (freed with its stream).
+struct DevScratch {
+  hipStream_t s = nullptr;
+  std::vector<void*> p;
+  ~DevScratch() {
+    if (s) (void)hipStreamSynchronize(s);
+    for (void* q : p) (void)hipFree(q);
+    if (s) (void)hipStreamDestroy(s);
+  }
+  template <typename T>
+  int alloc(T** q, int64_t n) {
+    MR_HIP(hipMalloc((void**)q, (size_t)std::max<int64_t>(n, 1) * sizeof(T)));
+    p.push_back(*q);
+    return 0;
+  }
+};
 }  // namespace
 
 extern "C" {
@@ -172,7 +188,8 @@ int mr_als_set_comm(mr_als* ctx, const mr_comm* comm, const long long* user_begi
     ctx->eng.has_comm = true;
     ctx->eng.row_begin_u.assign(user_begin, user_begin + comm->world + 1);
     ctx->eng.row_begin_i.assign(item_begin, item_begin + comm->world + 1);
-    return 0;
+    // the padded all-gather staging the RCCL transport uses, too
+    return comm->world > 1 ? ctx->eng.alloc_ag(comm->world) : 0;
   });
 }
 
@@ -239,7 +256,12 @@ int mr_als_set_option(mr_als* ctx, int option, double value) {
   MR_CHECK(ctx, "null context");
   switch (option) {
     case MR_OPT_FUSE_START: ctx->eng.fuse_start = value != 0.0; return 0;
-    case MR_OPT_CG_SPECULATE: ctx->eng.speculate = (int)value; return 0;
+    case MR_OPT_CG_SPECULATE:
+      // every rank of a sharded run must use the same level (it decides which
+      // launches, and with them which collectives, are issued)
+      MR_CHECK(value == 0.0 || value == 1.0 || value == 2.0, "cg_speculate must be 0, 1 or 2");
+      ctx->eng.speculate = (int)value;
+      return 0;
     case MR_OPT_WAIT_TIMEOUT_S:
       MR_CHECK(value > 0.0, "timeout must be > 0");
       ctx->eng.wait_timeout_s = value;
@@ -297,6 +319,17 @@ int mr_als_get_cg_vectors(mr_als* ctx, int side, double* r, double* p, double* q
   MR_CHECK(ctx, "null context");
   MR_CHECK(side == MR_SIDE_USERS || side == MR_SIDE_ITEMS, "unknown side");
   return guarded([&]() { return ctx->eng.get_cg_vectors(side == MR_SIDE_USERS, r, p, q); });
+}
+
+int mr_als_local_size(mr_als* ctx, int side, long long* first, long long* count,
+                      long long* nnz) {
+  MR_CHECK(ctx, "null context");
+  MR_CHECK(side == MR_SIDE_USERS || side == MR_SIDE_ITEMS, "unknown side");
+  const mr::Side& S = side == MR_SIDE_USERS ? ctx->eng.su : ctx->eng.si;
+  if (first) *first = S.e0;
+  if (count) *count = S.E;
+  if (nnz) *nnz = S.nnz;
+  return 0;
 }
 
 long long mr_als_work_items(mr_als* ctx, int side) {
@@ -363,6 +396,65 @@ int mr_als_predict(mr_als* ctx, long long n, const int* user_ids, const int* ite
                    double* out) {
   MR_CHECK(ctx, "null context");
   return guarded([&]() { return ctx->eng.predict(n, user_ids, item_ids, out); });
+}
+
+// ---- test hooks: the all-gather staging kernels on host arrays ----------------
+
+int mr_test_pack_rows(int device, long long rows, int ldk, const float* fac, const float* bias,
+                      long long r0, long long n, float* send, float* send_b) {
+  return guarded([&]() -> int {
+    MR_CHECK(ldk > 0 && ldk % 4 == 0, "ldk must be a positive multiple of 4");
+    MR_CHECK(rows >= 0 && r0 >= 0 && n >= 0 && r0 + n <= rows, "row range outside the table");
+    MR_HIP(hipSetDevice(device));
+    DevScratch d;
+    MR_HIP(hipStreamCreateWithFlags(&d.s, hipStreamNonBlocking));
+    float *dfac, *dbias = nullptr, *dsend, *dsend_b = nullptr;
+    if (d.alloc(&dfac, rows * ldk) || d.alloc(&dsend, n * ldk)) return -1;
+    if (bias && (d.alloc(&dbias, rows) || d.alloc(&dsend_b, n))) return -1;
+    MR_H2D(dfac, fac, rows * ldk * 4, d.s);
+    if (bias) MR_H2D(dbias, bias, rows * 4, d.s);
+    if (mr::launch_pack_rows(d.s, r0, n, ldk, dfac, dbias, dsend, dsend_b)) return -1;
+    MR_D2H(send, dsend, n * ldk * 4, d.s);
+    if (bias) MR_D2H(send_b, dsend_b, n * 4, d.s);
+    return 0;
+  });
+}
+
+int mr_test_unstage_rows(int device, int world, int skip, const long long* rb, long long maxrows,
+                         int ldk, const float* recv, const float* recv_b, float* fac,
+                         float* bias) {
+  return guarded([&]() -> int {
+    MR_CHECK(world >= 1 && skip >= -1 && skip < world, "bad world / skip");
+    MR_CHECK(ldk > 0 && ldk % 4 == 0, "ldk must be a positive multiple of 4");
+    MR_CHECK(rb[0] == 0 && maxrows >= 1, "bad row boundaries");
+    for (int r = 0; r < world; ++r)
+      MR_CHECK(rb[r + 1] >= rb[r] && rb[r + 1] - rb[r] <= maxrows,
+               "row boundaries not monotone or a shard exceeds maxrows");
+    const int64_t rows = rb[world];
+    MR_HIP(hipSetDevice(device));
+    DevScratch d;
+    MR_HIP(hipStreamCreateWithFlags(&d.s, hipStreamNonBlocking));
+    float *dfac, *dbias = nullptr, *drecv, *drecv_b = nullptr;
+    int64_t* drb;
+    if (d.alloc(&dfac, rows * ldk) || d.alloc(&drecv, (int64_t)world * maxrows * ldk) ||
+        d.alloc(&drb, world + 1))
+      return -1;
+    if (bias && (d.alloc(&dbias, rows) || d.alloc(&drecv_b, (int64_t)world * maxrows))) return -1;
+    std::vector<int64_t> rb64(rb, rb + world + 1);
+    MR_H2D(drb, rb64.data(), (world + 1) * 8, d.s);
+    MR_H2D(dfac, fac, rows * ldk * 4, d.s);
+    MR_H2D(drecv, recv, (int64_t)world * maxrows * ldk * 4, d.s);
+    if (bias) {
+      MR_H2D(dbias, bias, rows * 4, d.s);
+      MR_H2D(drecv_b, recv_b, (int64_t)world * maxrows * 4, d.s);
+    }
+    if (mr::launch_unstage_rows(d.s, world, skip, drb, maxrows, ldk, drecv, drecv_b, dfac,
+                                dbias))
+      return -1;
+    MR_D2H(fac, dfac, rows * ldk * 4, d.s);
+    if (bias) MR_D2H(bias, dbias, rows * 4, d.s);
+    return 0;
+  });
 }
 
 const char* mr_last_error(void) { return mr::last_error(); }

@@ -96,6 +96,7 @@ struct Engine {
   mr_comm comm{};
   std::vector<long long> row_begin_u, row_begin_i;
   AgStage ag_u, ag_i;
+  std::vector<float> h_ag;   // host staging of the padded exchange (callback transport)
 
   ~Engine();
   int init(int dev, int k, int64_t U, int64_t I, int64_t n_u, const int* uv_uid,
@@ -112,6 +113,11 @@ struct Engine {
   // single-rank) or host callbacks with more than one rank.
   bool sharded() const { return rccl != nullptr || (has_comm && comm.world > 1); }
   int set_rccl(const unsigned char* id, int rank, int world);
+  // padded all-gather staging (both transports): every shard padded to the
+  // largest one; needs row_begin_u / row_begin_i
+  int alloc_ag(int world);
+  int ag_world() const { return rccl ? rccl_world : comm.world; }
+  int ag_rank() const { return rccl ? rccl_rank : comm.rank; }
   int allreduce_state_slot(int count = 1);
   int allgather_side(bool user);
   int finalize_sharded(int phase, int seq);

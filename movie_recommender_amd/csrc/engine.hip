@@ -452,7 +452,15 @@ int Engine::set_rccl(const unsigned char* id, int rank, int world) {
   rccl = (void*)c;
   rccl_world = world;
   rccl_rank = rank;
-  // all-gather staging: every rank's shard padded to the largest one
+  return alloc_ag(world);
+}
+
+// All-gather staging, the same for both transports: every rank's shard padded
+// to the largest one (maxrows rows of ldk floats, + the user bias column).
+// Row boundaries are checked here, on the host, against everything the pack /
+// unstage kernels assume (monotone, covering the table, own shard <= maxrows).
+int Engine::alloc_ag(int world) {
+  MR_HIP(hipSetDevice(device));
   for (int side = 0; side < 2; ++side) {
     const std::vector<long long>& rb = side == 0 ? row_begin_u : row_begin_i;
     MR_CHECK((int)rb.size() == world + 1 && rb[0] == 0 && rb[world] == (side == 0 ? U : I),
@@ -463,6 +471,8 @@ int Engine::set_rccl(const unsigned char* id, int rank, int world) {
       mx = std::max(mx, rb[r + 1] - rb[r]);
     }
     AgStage& A = side == 0 ? ag_u : ag_i;
+    dfree(A.send, stream); dfree(A.recv, stream); dfree(A.send_b, stream);
+    dfree(A.recv_b, stream); dfree(A.rb, stream);
     A.maxrows = mx;
     if (dalloc(&A.send, mx * ldk, stream) || dalloc(&A.recv, (int64_t)world * mx * ldk, stream) ||
         dalloc(&A.rb, world + 1, stream))
@@ -473,6 +483,11 @@ int Engine::set_rccl(const unsigned char* id, int rank, int world) {
     std::vector<int64_t> rb64(rb.begin(), rb.end());
     MR_H2D(A.rb, rb64.data(), rb64.size() * 8, stream);
   }
+  // this rank's shard must be the one the context was built for
+  const int rk = ag_rank();
+  MR_CHECK(row_begin_u[rk] == su.e0 && row_begin_u[rk + 1] == su.e0 + su.E &&
+               row_begin_i[rk] == si.e0 && row_begin_i[rk + 1] == si.e0 + si.E,
+           "row boundaries disagree with this context's shard ranges");
   return 0;
 }
 
@@ -493,21 +508,27 @@ int Engine::allreduce_state_slot(int count) {
   return 0;
 }
 
-// Replicate the freshly solved shard rows of a factor table on every rank.
-// RCCL: ONE ncclAllGather of equal, padded shards (maxrows rows each): the
-// own rows are packed into a send buffer, gathered into world x maxrows rows,
-// and every other rank's rows unpacked into place by one kernel (users: the
-// bias column likewise, a second all-gather of maxrows floats).
+// Replicate the freshly solved shard rows of a factor table on every rank:
+// the own rows are packed into a send buffer, exchanged as ONE all-gather of
+// equal, padded shards (world x maxrows rows), and every other rank's rows
+// unstaged into place by one kernel (users: the bias column likewise).  The
+// device side (pack_rows -> padded buffers -> unstage_rows) is the same for
+// both transports: RCCL gathers the device buffers directly; the callback
+// transport carries the same padded buffers through host memory and
+// comm.allgather_rows (padded row boundaries r * maxrows), so the gloo tests
+// run the exact staging code of the RCCL path at any world size.
 int Engine::allgather_side(bool user) {
   if (!sharded()) return 0;
   const std::vector<long long>& rb = user ? row_begin_u : row_begin_i;
+  const int world = ag_world(), rank = ag_rank();
+  AgStage& A = user ? ag_u : ag_i;
+  MR_CHECK(A.recv != nullptr, "all-gather staging not allocated");
+  float* fac = user ? Ufac : Vfac;
+  float* bias = user ? Ubias : nullptr;
+  if (launch_pack_rows(stream, rb[rank], rb[rank + 1] - rb[rank], ldk, fac, bias, A.send,
+                       A.send_b))
+    return -1;
   if (rccl) {
-    AgStage& A = user ? ag_u : ag_i;
-    float* fac = user ? Ufac : Vfac;
-    float* bias = user ? Ubias : nullptr;
-    if (launch_pack_rows(stream, rb[rccl_rank], rb[rccl_rank + 1] - rb[rccl_rank], ldk, fac,
-                         bias, A.send, A.send_b))
-      return -1;
     MR_NCCL(ncclGroupStart());
     MR_NCCL(ncclAllGather(A.send, A.recv, (size_t)(A.maxrows * ldk), ncclFloat,
                           (ncclComm_t)rccl, stream));
@@ -515,33 +536,25 @@ int Engine::allgather_side(bool user) {
       MR_NCCL(ncclAllGather(A.send_b, A.recv_b, (size_t)A.maxrows, ncclFloat, (ncclComm_t)rccl,
                             stream));
     MR_NCCL(ncclGroupEnd());
-    return launch_unstage_rows(stream, rccl_world, rccl_rank, A.rb, A.maxrows, ldk, A.recv,
-                               A.recv_b, fac, bias);
+  } else {
+    const int64_t per = A.maxrows * ldk;
+    h_ag.resize((size_t)world * per + (user ? (size_t)world * A.maxrows : 0));
+    float* tab = h_ag.data();
+    float* tab_b = tab + (size_t)world * per;
+    MR_D2H(tab + (size_t)rank * per, A.send, per * 4, stream);
+    if (user) MR_D2H(tab_b + (size_t)rank * A.maxrows, A.send_b, A.maxrows * 4, stream);
+    std::vector<long long> prb(world + 1);
+    for (int r = 0; r <= world; ++r) prb[r] = (long long)r * A.maxrows;
+    MR_CHECK(comm.allgather_rows(comm.user, tab, ldk, prb.data(), world) == 0,
+             "allgather callback failed");
+    if (user)
+      MR_CHECK(comm.allgather_rows(comm.user, tab_b, 1, prb.data(), world) == 0,
+               "allgather callback failed");
+    MR_H2D(A.recv, tab, (size_t)world * per * 4, stream);
+    if (user) MR_H2D(A.recv_b, tab_b, (size_t)world * A.maxrows * 4, stream);
   }
-  const int64_t rows = user ? U : I;
-  // gather [fac | bias] rows through host staging
-  const int64_t rowf = user ? ldk + 1 : ldk;
-  std::vector<float> tab(rows * rowf);
-  std::vector<float> fac(rows * ldk), bias(user ? rows : 0);
-  MR_D2H(fac.data(), user ? Ufac : Vfac, rows * ldk * 4, stream);
-  if (user)
-    MR_D2H(bias.data(), Ubias, rows * 4, stream);
-  MR_HIP(hipStreamSynchronize(stream));
-  for (int64_t r = 0; r < rows; ++r) {
-    memcpy(&tab[r * rowf], &fac[r * ldk], ldk * 4);
-    if (user) tab[r * rowf + ldk] = bias[r];
-  }
-  MR_CHECK(comm.allgather_rows(comm.user, tab.data(), rowf, rb.data(), comm.world) == 0,
-           "allgather callback failed");
-  for (int64_t r = 0; r < rows; ++r) {
-    memcpy(&fac[r * ldk], &tab[r * rowf], ldk * 4);
-    if (user) bias[r] = tab[r * rowf + ldk];
-  }
-  MR_H2D(user ? Ufac : Vfac, fac.data(), rows * ldk * 4, stream);
-  if (user)
-    MR_H2D(Ubias, bias.data(), rows * 4, stream);
-  MR_HIP(hipStreamSynchronize(stream));
-  return 0;
+  return launch_unstage_rows(stream, world, rank, A.rb, A.maxrows, ldk, A.recv, A.recv_b, fac,
+                             bias);
 }
 
 // Sharded CG: all-reduce the slot the last block filled, then apply the rule.

@@ -732,9 +732,33 @@ __device__ __forceinline__ void bf3_split(u32x4_t (&P)[3][NB], float (&cacc)[NB]
 
 // hh, hm, mh, hl, lh, mm over the NB(NB+1)/2 upper blocks, product-major
 // (consecutive MFMAs write different accumulators: no dependency stalls).
+// Wait states around the inline-asm MFMAs (NB >= 5).  LLVM's hazard
+// recognizer sees an asm statement as an opaque instruction, so it inserts
+// none of the gfx950 MFMA wait states for it; these guards make them explicit
+// instead of relying on the surrounding code's length:
+//   * before the first MFMA of a half: VALU writes of P (the split) and of the
+//     accumulators (their zeroing) -> MFMA SrcA/B/C reads need <= 2 wait
+//     states on gfx940+; s_nop 4 gives 5;
+//   * after the last MFMA, before the epilogue reads the accumulators: an
+//     8-pass XDL result -> VALU / v_accvgpr_read needs NumPasses + 3 (+1 on
+//     gfx950) = 12 wait states; three s_nop give 8 + 8 + 4 = 20.
+// sched_barrier(0) on both sides keeps the scheduler from moving any
+// instruction across a guard.
+__device__ __forceinline__ void mfma_entry_guard() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 4");
+  __builtin_amdgcn_sched_barrier(0);
+}
+__device__ __forceinline__ void mfma_exit_guard() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 template <int NB>
 __device__ __forceinline__ void bf3_mfma(floatx4 (&acc)[NB * (NB + 1) / 2],
                                          const u32x4_t (&P)[3][NB]) {
+  if constexpr (NB >= 5) mfma_entry_guard();
 #pragma unroll
   for (int sidx = 0; sidx < 6; ++sidx) {
     const int pa = (sidx == 2) ? 1 : (sidx == 4) ? 2 : (sidx == 5) ? 1 : 0;
@@ -750,10 +774,8 @@ __device__ __forceinline__ void bf3_mfma(floatx4 (&acc)[NB * (NB + 1) / 2],
           // in VGPRs inside the loop and copied them to / from AGPRs every
           // half (200 v_accvgpr_* per half at NB = 8; loop 984 -> 783
           // instructions; k = 128 Gram users 1313 -> 1255 us, items 1001 ->
-          // 960 us same-box, bit-identical).  The hazard windows are covered
-          // by the code around the loop: the split's ~500 VALU separate the
-          // last MFMA from the epilogue's accumulator reads, and the gathers
-          // separate the split's P writes from the next MFMAs.
+          // 960 us same-box, bit-identical).  Hazard wait states: explicit
+          // guards (mfma_entry_guard above, mfma_exit_guard after the loop).
           asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
               : "+a"(acc[t]) : "v"(P[pa][bi]), "v"(P[pb][bj]));
         } else {
@@ -861,6 +883,7 @@ __device__ __forceinline__ void gram_wave(
     h1 = h2;
     h2 = h3;
   }
+  if constexpr (NB >= 5) mfma_exit_guard();
 
   // ---- epilogue -----------------------------------------------------------
 #pragma unroll

@@ -54,13 +54,20 @@ def entity_cost(counts, k, cg_iterations=6):
     return counts + c
 
 
-def shard_views(user_ids, item_ids, ratings, num_users, num_items, rank, world, k=None):
+def shard_views(user_ids, item_ids, ratings, num_users, num_items, rank, world, k=None,
+                bounds=None):
     """(user_range, item_range, user_view, item_view, ub, ib) for ``rank``;
-    with ``k`` the boundaries balance ``entity_cost``, else rating counts."""
-    uc = np.bincount(user_ids, minlength=num_users)
-    ic = np.bincount(item_ids, minlength=num_items)
-    ub = shard_bounds(entity_cost(uc, k), world)
-    ib = shard_bounds(entity_cost(ic, k), world)
+    with ``k`` the boundaries balance ``entity_cost``, else rating counts;
+    ``bounds=(ub, ib)`` imposes them (tests of uneven shards)."""
+    if bounds is not None:
+        ub, ib = (np.asarray(b, np.int64) for b in bounds)
+        assert len(ub) == len(ib) == world + 1
+        assert ub[0] == 0 and ub[-1] == num_users and ib[0] == 0 and ib[-1] == num_items
+    else:
+        uc = np.bincount(user_ids, minlength=num_users)
+        ic = np.bincount(item_ids, minlength=num_items)
+        ub = shard_bounds(entity_cost(uc, k), world)
+        ib = shard_bounds(entity_cost(ic, k), world)
     u0, u1 = int(ub[rank]), int(ub[rank + 1])
     i0, i1 = int(ib[rank]), int(ib[rank + 1])
     su = (user_ids >= u0) & (user_ids < u1)
@@ -146,15 +153,17 @@ def attach_rccl(ctx, rank, world, user_begin, item_begin):
 
 
 def sharded_context(user_ids, item_ids, ratings, k, num_users, num_items, device,
-                    comm="rccl", **kw):
+                    comm="rccl", bounds=None, **kw):
     """Build this rank's ``AlsContext`` over an initialised torch.distributed
     group and attach its collectives: ``comm="rccl"`` (native, device-side),
-    or a ``TorchComm`` (host-staged callbacks; works with gloo)."""
+    or a ``TorchComm`` (host-staged callbacks carrying the same padded
+    exchange buffers; works with gloo).  ``bounds=(ub, ib)`` imposes the
+    shard boundaries (default: cost-balanced)."""
     import torch.distributed as dist
     from .engine import AlsContext
     rank, world = dist.get_rank(), dist.get_world_size()
     (u0, u1), (i0, i1), uv, iv, ub, ib = shard_views(
-        user_ids, item_ids, ratings, num_users, num_items, rank, world, k=k)
+        user_ids, item_ids, ratings, num_users, num_items, rank, world, k=k, bounds=bounds)
     ctx = AlsContext(uv[0], uv[1], uv[2], k, num_users, num_items, device=device,
                      user_range=(u0, u1), item_range=(i0, i1), item_view=iv, **kw)
     if comm == "rccl":

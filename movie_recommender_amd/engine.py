@@ -175,17 +175,26 @@ class AlsContext:
             G.ctypes.data_as(_lib.DP), c.ctypes.data_as(_lib.DP)), "mr_als_get_normal_equations")
         return G, c
 
+    def local_size(self, side):
+        """(first global id, count, ratings held) of this context's entities
+        of ``side`` (a shard owns a contiguous range)."""
+        v = [ctypes.c_longlong(0) for _ in range(3)]
+        _lib.check(_lib.lib().mr_als_local_size(self._h, 0 if side in (0, "users") else 1,
+                                                *[ctypes.byref(x) for x in v]),
+                   "mr_als_local_size")
+        return tuple(int(x.value) for x in v)
+
     def layout(self, side):
         """The side's device CSR (off, idx, val) and Gram work list
-        (begin, len, entity, slab) as built on the GPU."""
+        (begin, len, entity, slab) as built on the GPU (local entities)."""
         L = _lib.lib()
         user = side in (0, "users")
         sd = 0 if user else 1
-        E = self.num_users if user else self.num_items
+        _, E, nnz = self.local_size(side)
         off = np.empty(E + 1, np.int64)
         _lib.check(L.mr_als_get_layout(self._h, sd, off.ctypes.data_as(_lib.LLP), None, None,
                                        None, None, None, None), "mr_als_get_layout")
-        nnz = int(off[-1])
+        assert int(off[-1]) == nnz
         nw = int(L.mr_als_work_items(self._h, sd))
         idx = np.empty(nnz, np.int32)
         val = np.empty(nnz, np.float32)
@@ -198,9 +207,11 @@ class AlsContext:
         return off, idx, val, (wb, wl, we, ws)
 
     def cg_vectors(self, side):
-        """(r, p, q) of the side's last CG solve, fp64 (users: k+1 per user)."""
+        """(r, p, q) of the side's last CG solve over the local entities, fp64
+        (users: k+1 per user)."""
         user = side in (0, "users")
-        n = (self.num_users * (self.k + 1)) if user else (self.num_items * self.k)
+        _, E, _ = self.local_size(side)
+        n = E * (self.k + 1) if user else E * self.k
         out = [np.empty(n) for _ in range(3)]
         _lib.check(_lib.lib().mr_als_get_cg_vectors(
             self._h, 0 if user else 1, *[a.ctypes.data_as(_lib.DP) for a in out]),

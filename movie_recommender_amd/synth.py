@@ -39,6 +39,7 @@ class RatingSet:
     test_user_ids: np.ndarray = field(default=None)
     test_item_ids: np.ndarray = field(default=None)
     test_ratings: np.ndarray = field(default=None)
+    medians: np.ndarray = field(default=None)   # per (compact) item: train-split median
     meta: dict = field(default_factory=dict)
 
     @property
@@ -143,6 +144,7 @@ def movielens_like(shape="ml-full", k=64, seed=DATA_SEED, model="lowrank",
     imap[ii] = np.arange(len(ii))
     rs = RatingSet(umap[tu].astype(np.int32), imap[ti].astype(np.int32),
                    (tr - med[ti]).astype(np.float64), len(uu), len(ii), k)
+    rs.medians = med[ii]
     if test_ratio > 0:
         hu, hi_, hr = u[test], i[test], r[test]
         ok = (umap[hu] >= 0) & (imap[hi_] >= 0)

@@ -319,3 +319,34 @@ def predict(U, V, user_ids, item_ids, k):
 def rmse(U, V, user_ids, item_ids, ratings, k):
     d = predict(U, V, user_ids, item_ids, k) - np.asarray(ratings, np.float64)
     return float(np.sqrt(np.mean(d * d)))
+
+
+def rank_agreement_mean(U, V, k, user_ids, item_ids, ratings, medians):
+    """Mean per-user ranking agreement on held-out ratings, the reference's
+    quality metric (``_als_eval``, ``python/full_data/worker_process.py:262-306``
+    with ``compute_ranking_agreement``, ``my_util.py:101-145``): each test
+    user's movies are scored ``u[:k].v + u[k] + median`` (``als_predictor.py:
+    35-60``) and compared with the raw ratings (residual + median); over
+    every pair with actual(m1) > actual(m2), agreement when predicted(m1) >
+    predicted(m2).  Users with one rating or all-equal ratings have no
+    agreement (None in the reference) and are skipped.  Returns (mean over
+    users with an agreement, number of such users)."""
+    med = np.asarray(medians, np.float64)
+    pred = predict(U, V, user_ids, item_ids, k) + med[item_ids]
+    act = np.asarray(ratings, np.float64) + med[item_ids]
+    order = np.argsort(user_ids, kind="stable")
+    u_s, p_s, a_s = np.asarray(user_ids)[order], pred[order], act[order]
+    bounds = np.flatnonzero(np.diff(u_s)) + 1
+    starts = np.concatenate([[0], bounds])
+    ends = np.concatenate([bounds, [len(u_s)]])
+    vals = []
+    for s, e in zip(starts, ends):
+        if e - s < 2:
+            continue
+        a, p = a_s[s:e], p_s[s:e]
+        gt = a[:, None] > a[None, :]
+        n = int(np.count_nonzero(gt))
+        if n == 0:
+            continue
+        vals.append(np.count_nonzero(gt & (p[:, None] > p[None, :])) / n)
+    return (float(np.mean(vals)) if vals else float("nan")), len(vals)

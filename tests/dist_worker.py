@@ -8,7 +8,9 @@ Modes
                equations, all-reduced CG scalars, all-gathered factor shards)
                restated with the NumPy oracle over gloo; rank 0 saves U, V, ret.
   engine_gloo  the HIP engine, one shard context per rank (all on cuda:0 when
-               the box has one GPU), collectives through TorchComm callbacks.
+               the box has one GPU), collectives through TorchComm callbacks
+               (the same padded device exchange buffers as RCCL: pack_rows
+               -> all-gather -> unstage_rows); --skew imposes uneven shards.
   engine_rccl  the HIP engine with its native RCCL communicator.
 """
 import argparse
@@ -78,15 +80,26 @@ def oracle_sharded(d, max_iteration, rank, world):
     return U, V, it
 
 
-def engine_sharded(d, max_iteration, rank, world, mode):
+def skewed_bounds(n, world):
+    """Deliberately uneven shards (rank r's share grows as 2^r): the padded
+    exchange then carries mostly padding for the small ranks."""
+    w = 2.0 ** np.arange(world)
+    b = np.concatenate([[0], np.floor(np.cumsum(w) / w.sum() * n)]).astype(np.int64)
+    b[-1] = n
+    return b
+
+
+def engine_sharded(d, max_iteration, rank, world, mode, skew=False):
     import torch.distributed as dist
     from movie_recommender_amd.distributed import TorchComm, sharded_context
     from movie_recommender_amd.engine import device_count
     k = int(d["k"])
     dev = rank % max(1, device_count())
     comm = "rccl" if mode == "engine_rccl" else TorchComm()
-    ctx = sharded_context(d["user_ids"], d["item_ids"], d["ratings"], k,
-                          int(d["num_users"]), int(d["num_items"]), dev, comm)
+    nU, nI = int(d["num_users"]), int(d["num_items"])
+    bounds = (skewed_bounds(nU, world), skewed_bounds(nI, world)) if skew else None
+    ctx = sharded_context(d["user_ids"], d["item_ids"], d["ratings"], k, nU, nI, dev, comm,
+                          bounds=bounds)
     ctx.set_factors(d["U0"], d["V0"])
     ret = ctx.run(0.01, max_iteration)
     U, V = ctx.get_factors()
@@ -95,21 +108,51 @@ def engine_sharded(d, max_iteration, rank, world, mode):
     return U, V, ret
 
 
+def comm_padded(rank, world):
+    """The callback transport's host side as the engine drives it: the padded
+    exchange table (world x maxrows rows, this rank's packed block at
+    rank x maxrows) through TorchComm's allgather_rows with padded row
+    boundaries, then the bias column (1 float per row); returns the gathered
+    tables for rank 0 to compare with the expected blocks."""
+    import ctypes
+    from movie_recommender_amd.distributed import TorchComm
+    comm = TorchComm()
+    maxrows, ldk = 5, 8
+    tab = np.full(world * maxrows * ldk, -1.0, np.float32)
+    tab_b = np.full(world * maxrows, -1.0, np.float32)
+    mine = slice(rank * maxrows * ldk, (rank + 1) * maxrows * ldk)
+    tab[mine] = 1000 * rank + np.arange(maxrows * ldk)
+    tab_b[rank * maxrows:(rank + 1) * maxrows] = 1000 * rank + np.arange(maxrows) + 0.5
+    prb = np.arange(world + 1, dtype=np.int64) * maxrows
+    fp = ctypes.POINTER(ctypes.c_float)
+    llp = ctypes.POINTER(ctypes.c_longlong)
+    rc1 = comm.struct.allgather_rows(None, tab.ctypes.data_as(fp), ldk,
+                                     prb.ctypes.data_as(llp), world)
+    rc2 = comm.struct.allgather_rows(None, tab_b.ctypes.data_as(fp), 1,
+                                     prb.ctypes.data_as(llp), world)
+    assert rc1 == 0 and rc2 == 0, comm.errors
+    return tab, tab_b
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mode", required=True)
     ap.add_argument("--fixture", required=True)
     ap.add_argument("--max-iteration", type=int, default=200)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--skew", action="store_true", help="uneven shard boundaries")
     a = ap.parse_args()
     import torch.distributed as dist
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     d = load(a.fixture)
-    if a.mode == "oracle":
+    if a.mode == "comm_padded":
+        U, V = comm_padded(rank, world)
+        ret = world
+    elif a.mode == "oracle":
         U, V, ret = oracle_sharded(d, a.max_iteration, rank, world)
     else:
-        U, V, ret = engine_sharded(d, a.max_iteration, rank, world, a.mode)
+        U, V, ret = engine_sharded(d, a.max_iteration, rank, world, a.mode, a.skew)
     if rank == 0:
         np.savez(a.out, U=U, V=V, ret=ret)
     dist.barrier()

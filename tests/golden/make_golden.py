@@ -321,6 +321,66 @@ def g8():
     print("G8 test rmse", tr.min(), tr.max(), "train", trn.min(), trn.max())
 
 
+def g9():
+    """G4 at the headline shape, round 3: the band of ``g8`` regenerated from
+    5 initial-factor seeds x thread counts {1, 2, 4, 8} (20 reference runs;
+    SURVEY.md 8(c) asks for >= 15), each run with its held-out RMSE, train
+    RMSE, ``ret`` and the reference's own quality metric, the mean per-user
+    ranking agreement on the held-out 20 % (``worker_process.py:262-306`` +
+    ``my_util.py:101-145``, restated in ``als_oracle.rank_agreement_mean``).
+    Runs are appended to a partial file as they finish (a 1-thread run takes
+    minutes), so an interrupted generation resumes."""
+    k, mi = 64, 4
+    rs_ = synth.movielens_like("ml-full", k, seed=synth.DATA_SEED, test_ratio=0.2)
+    part = os.path.join("/tmp", "band_mlfull_k64_g9.partial.json")
+    runs = []
+    if os.path.exists(part):
+        with open(part) as f:
+            runs = json.load(f)
+    done = {(r["seed"], r["tc"]) for r in runs}
+    for seed in range(5):
+        U0, V0 = ref.init_factors(rs_.num_users, rs_.num_items, k, seed)
+        for tc in (8, 4, 2, 1):
+            if (seed, tc) in done:
+                continue
+            ref.set_thread_count(tc)
+            t0 = __import__("time").perf_counter()
+            U, V, ret = ref.als(rs_.user_ids, rs_.item_ids, rs_.ratings, k, U0, V0,
+                                max_iteration=mi)
+            wall = __import__("time").perf_counter() - t0
+            agr, n_agr = als_oracle.rank_agreement_mean(
+                U, V, k, rs_.test_user_ids, rs_.test_item_ids, rs_.test_ratings, rs_.medians)
+            runs.append(dict(
+                seed=seed, tc=tc, ret=ret, wall_s=round(wall, 1),
+                train_rmse=als_oracle.rmse(U, V, rs_.user_ids, rs_.item_ids, rs_.ratings, k),
+                test_rmse=als_oracle.rmse(U, V, rs_.test_user_ids, rs_.test_item_ids,
+                                          rs_.test_ratings, k),
+                rank_agreement=agr, n_agreement_users=n_agr))
+            print("G9 run", runs[-1], flush=True)
+            with open(part, "w") as f:
+                json.dump(runs, f)
+    tr = np.array([r["test_rmse"] for r in runs])
+    trn = np.array([r["train_rmse"] for r in runs])
+    ag = np.array([r["rank_agreement"] for r in runs])
+    band = dict(shape="ml-full", k=k, max_iteration=mi, data_seed=synth.DATA_SEED,
+                test_ratio=0.2, n_train=int(rs_.n), n_test=int(len(rs_.test_ratings)),
+                num_users=rs_.num_users, num_items=rs_.num_items,
+                ratings_checksum=float(np.sum(rs_.ratings)),
+                medians_checksum=float(np.sum(rs_.medians)), runs=runs,
+                test_rmse_min=float(tr.min()), test_rmse_max=float(tr.max()),
+                test_rmse_mean=float(tr.mean()), test_rmse_std=float(tr.std()),
+                train_rmse_min=float(trn.min()), train_rmse_max=float(trn.max()),
+                train_rmse_mean=float(trn.mean()), train_rmse_std=float(trn.std()),
+                rank_agreement_min=float(ag.min()), rank_agreement_max=float(ag.max()),
+                rank_agreement_mean=float(ag.mean()), rank_agreement_std=float(ag.std()),
+                meta=_meta(None))
+    with open(os.path.join(HERE, "band_mlfull_k64.json"), "w") as f:
+        json.dump(band, f, indent=1)
+    ref.set_thread_count(1)
+    print("G9 test rmse", tr.min(), tr.max(), "train", trn.min(), trn.max(),
+          "agreement", ag.min(), ag.max())
+
+
 if __name__ == "__main__":
     steps = sys.argv[1:] or ["g1", "g2", "g3", "g4", "g5", "g6", "g7", "g8"]
     for s in steps:

@@ -22,13 +22,13 @@ def free_port():
     return p
 
 
-def run_workers(mode, fixture, nproc, tmp_path, max_iteration=200, timeout=600):
-    out = str(tmp_path / f"{mode}_{nproc}.npz")
+def run_workers(mode, fixture, nproc, tmp_path, max_iteration=200, timeout=600, skew=False):
+    out = str(tmp_path / f"{mode}_{nproc}{'_skew' if skew else ''}.npz")
     env = dict(os.environ, OMP_NUM_THREADS="2", MR_QUIET="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1",
            f"--master-port={free_port()}", WORKER, "--mode", mode, "--fixture", fixture,
-           "--max-iteration", str(max_iteration), "--out", out]
+           "--max-iteration", str(max_iteration), "--out", out] + (["--skew"] if skew else [])
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env,
                        cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
@@ -114,19 +114,53 @@ def test_sharded_algorithm_gloo_cpu_world3(tmp_path):
     assert rel_err(U, Uo) < tol and rel_err(V, Vo) < tol
 
 
+def test_callback_transport_padded_exchange_gloo_cpu(tmp_path):
+    """World size 3 on CPU: the host side of the callback transport exactly as
+    the engine drives it (Engine::allgather_side) -- each rank's packed block
+    at rank x maxrows of the padded table, TorchComm.allgather_rows with
+    padded row boundaries, factor rows and then the bias column -- gives
+    every rank every block."""
+    world, maxrows, ldk = 3, 5, 8
+    tab, tab_b, ret = run_workers("comm_padded", "als_dense_38x45_k5.npz", world, tmp_path)
+    assert ret == world
+    for r in range(world):
+        blk = tab[r * maxrows * ldk:(r + 1) * maxrows * ldk]
+        assert np.array_equal(blk, 1000 * r + np.arange(maxrows * ldk, dtype=np.float32))
+        assert np.array_equal(tab_b[r * maxrows:(r + 1) * maxrows],
+                              1000 * r + np.arange(maxrows, dtype=np.float32) + 0.5)
+
+
+def test_skewed_bounds_cover_and_grow():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from dist_worker import skewed_bounds
+    for n, world in ((300, 3), (260, 2), (50, 8)):
+        b = skewed_bounds(n, world)
+        assert b[0] == 0 and b[-1] == n and np.all(np.diff(b) >= 0)
+        assert np.diff(b)[-1] > np.diff(b)[0]
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("fixture,max_it", [("als_dense_300x200_k10.npz", 200),
-                                            ("als_dense_300x260_k64.npz", 200),
-                                            ("als_mlshape_k64_it4.npz", 4),
-                                            ("als_dense_340x300_k144.npz", 3)])
-def test_engine_two_ranks_gloo_matches_single(gpu, tmp_path, fixture, max_it):
-    """The real engine sharded over 2 ranks (both on cuda:0 on a one-GPU box;
-    cost-balanced shards, all-reduced CG scalars, all-gathered factor shards)
-    against the single-context run and the compiled reference's golden."""
+@pytest.mark.parametrize("fixture,max_it,nproc,skew", [
+    ("als_dense_300x200_k10.npz", 200, 2, False),
+    ("als_dense_300x260_k64.npz", 200, 2, False),
+    ("als_mlshape_k64_it4.npz", 4, 2, False),
+    ("als_dense_340x300_k144.npz", 3, 2, False),
+    # round 3: world 3, uneven (2^r) shards, k = 64 and 128 -- the padded
+    # pack_rows -> all-gather -> unstage_rows exchange the RCCL path runs
+    ("als_dense_300x260_k64.npz", 200, 3, True),
+    ("als_mlshape_k64_it4.npz", 4, 3, False),
+    ("als_dense_400x300_k128.npz", 200, 2, False),
+    ("als_dense_400x300_k128.npz", 200, 3, True)])
+def test_engine_sharded_gloo_matches_single(gpu, tmp_path, fixture, max_it, nproc, skew):
+    """The real engine sharded over 2 or 3 ranks (all on cuda:0 on a one-GPU
+    box; cost-balanced or deliberately uneven shards, all-reduced CG scalars,
+    factor shards exchanged through the padded device buffers of the RCCL
+    path) against the single-context run and the compiled reference's
+    golden."""
     from movie_recommender_amd.engine import AlsContext
     d = load_golden(fixture)
     k, nU, nI = int(d["k"]), int(d["num_users"]), int(d["num_items"])
-    U, V, ret = run_workers("engine_gloo", fixture, 2, tmp_path, max_it)
+    U, V, ret = run_workers("engine_gloo", fixture, nproc, tmp_path, max_it, skew=skew)
     with AlsContext(d["user_ids"], d["item_ids"], d["ratings"], k, nU, nI) as ctx:
         ctx.set_factors(d["U0"], d["V0"])
         ret1 = ctx.run(0.01, max_it)
@@ -153,3 +187,79 @@ def test_engine_rccl_path_matches_single(gpu, tmp_path):
     if nproc == 1:
         assert np.array_equal(U, U1) and np.array_equal(V, V1)
     assert rel_err(U, d["U"]) < 1e-5 and rel_err(V, d["V"]) < 1e-5
+
+
+def _unstage_expected(world, skip, rb, maxrows, ldk, recv, recv_b, fac, bias):
+    fac = fac.copy()
+    bias = bias.copy() if bias is not None else None
+    for s in range(world):
+        if s == skip:
+            continue
+        n = rb[s + 1] - rb[s]
+        blk = recv.reshape(world, maxrows, ldk)[s, :n]
+        fac.reshape(-1, ldk)[rb[s]:rb[s] + n] = blk
+        if bias is not None:
+            bias[rb[s]:rb[s] + n] = recv_b.reshape(world, maxrows)[s, :n]
+    return fac, bias
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ldk,with_bias", [(64, True), (128, False), (16, True)])
+def test_unstage_rows_fabricated_world8(gpu, ldk, with_bias):
+    """unstage_rows_kernel (the RCCL path's receive side) on a fabricated
+    world = 8 receive buffer: uneven shards, two empty ones, the largest
+    defining maxrows, each rank in turn the skipped (own) one -- against a
+    NumPy restatement, bit for bit (a pure copy)."""
+    import ctypes
+    from movie_recommender_amd import _lib
+    L = _lib.lib()
+    world = 8
+    sizes = np.array([37, 0, 5, 64, 1, 0, 23, 41])
+    rb = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    maxrows = int(sizes.max())
+    rows = int(rb[-1])
+    rng = np.random.default_rng(ldk)
+    recv = rng.standard_normal(world * maxrows * ldk).astype(np.float32)
+    recv_b = rng.standard_normal(world * maxrows).astype(np.float32) if with_bias else None
+    fac0 = rng.standard_normal(rows * ldk).astype(np.float32)
+    bias0 = rng.standard_normal(rows).astype(np.float32) if with_bias else None
+    fp = lambda a: a.ctypes.data_as(_lib.FP) if a is not None else None  # noqa: E731
+    for skip in range(-1, world):
+        fac = fac0.copy()
+        bias = bias0.copy() if with_bias else None
+        _lib.check(L.mr_test_unstage_rows(0, world, skip, rb.ctypes.data_as(_lib.LLP), maxrows,
+                                          ldk, fp(recv), fp(recv_b), fp(fac), fp(bias)),
+                   "mr_test_unstage_rows")
+        ef, eb = _unstage_expected(world, skip, rb, maxrows, ldk, recv, recv_b, fac0, bias0)
+        assert np.array_equal(fac, ef)
+        if with_bias:
+            assert np.array_equal(bias, eb)
+    # shapes the kernel cannot take are refused on the host
+    bad = rb.copy()
+    bad[4] = bad[3] - 1
+    assert L.mr_test_unstage_rows(0, world, 0, bad.ctypes.data_as(_lib.LLP), maxrows, ldk,
+                                  fp(recv), fp(recv_b), fp(fac0.copy()),
+                                  fp(bias0.copy() if with_bias else None)) < 0
+    assert L.mr_test_unstage_rows(0, world, 0, rb.ctypes.data_as(_lib.LLP), maxrows - 1, ldk,
+                                  fp(recv), fp(recv_b), fp(fac0.copy()),
+                                  fp(bias0.copy() if with_bias else None)) < 0
+
+
+@pytest.mark.gpu
+def test_pack_rows_matches_slice(gpu):
+    """pack_rows_kernel (the send side): rows [r0, r0+n) and their bias."""
+    from movie_recommender_amd import _lib
+    L = _lib.lib()
+    rows, ldk = 300, 64
+    rng = np.random.default_rng(1)
+    fac = rng.standard_normal(rows * ldk).astype(np.float32)
+    bias = rng.standard_normal(rows).astype(np.float32)
+    for r0, n in ((0, 300), (17, 113), (299, 1), (120, 0)):
+        send = np.zeros(max(n, 1) * ldk, np.float32)
+        send_b = np.zeros(max(n, 1), np.float32)
+        _lib.check(L.mr_test_pack_rows(0, rows, ldk, fac.ctypes.data_as(_lib.FP),
+                                       bias.ctypes.data_as(_lib.FP), r0, n,
+                                       send.ctypes.data_as(_lib.FP),
+                                       send_b.ctypes.data_as(_lib.FP)), "mr_test_pack_rows")
+        assert np.array_equal(send[:n * ldk], fac[r0 * ldk:(r0 + n) * ldk])
+        assert np.array_equal(send_b[:n], bias[r0:r0 + n])

@@ -1,0 +1,211 @@
+"""BASELINE.json configs[3] and [4] on one GPU (round 3).
+
+* C4, MovieLens-full shape at k = 128 (the 8-GPU config's data set): the
+  context build, sampled normal equations and the first CG half-step of
+  each side at full size against host restatements / the oracle's CG on the
+  GPU's own normal equations.
+* C5, synthetic 10 M x 1 M x 1e9 at k = 128: one rank's slice of the
+  streamed generator (``synth.C5Generator.user_view`` / ``item_view``, the
+  views ``bench.py --shape c5`` builds per rank) as a shard context, the
+  device factor seeding (``mr_als_init_factors``) against a host restatement
+  of its hash, and the slice's normal equations and first half-step.
+
+The reference cannot run C5 at all (int32 overflow of N (k+1),
+``cpp/ls_lib/matrix.cpp:757-759``), so these properties and the oracle's CG
+are the evidence there."""
+import numpy as np
+import pytest
+
+from conftest import rel_err  # noqa: F401
+from test_gpu_parity import expected_layout
+
+pytestmark = pytest.mark.gpu
+
+
+# ---------------------------------------------------------------------------
+# host restatement of init_factors_kernel (kernels.hip): splitmix64 of the
+# (table, row, column) index, uniform(-1, 1), rounded to fp32
+# ---------------------------------------------------------------------------
+M64 = (1 << 64) - 1
+
+
+def _splitmix_unit(x):
+    x = (x + np.uint64(0x9E3779B97F4A7C15)) & np.uint64(M64)
+    x = ((x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)) & np.uint64(M64)
+    x = ((x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)) & np.uint64(M64)
+    x = x ^ (x >> np.uint64(31))
+    return (x >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0) * 2.0 - 1.0
+
+
+def init_factor_rows(seed, table, rows, k):
+    """Rows ``rows`` of table 0 (U: k factors + bias) or 1 (V: k factors)."""
+    width = k + 1 if table == 0 else k
+    with np.errstate(over="ignore"):
+        base = (np.uint64(seed) * np.uint64(0x100000001B3)) ^ (np.uint64(table) << np.uint64(60))
+        idx = (np.asarray(rows, np.uint64)[:, None] * np.uint64(k + 1)
+               + np.arange(width, dtype=np.uint64)[None, :])
+        return _splitmix_unit(base + idx).astype(np.float32).astype(np.float64)
+
+
+def _sampled_gram_check(ctx, side, ids, other, ratings, U, V, k, ents, tol=2e-5):
+    ctx.build_normal_equations(side)
+    G, c = ctx.normal_equations(side, ents)
+    Vm = V.reshape(-1, k)
+    Um = U.reshape(-1, k + 1)
+    order = np.argsort(ids, kind="stable")
+    ids_s = ids[order]
+    for t, e in enumerate(ents):
+        lo, hi = np.searchsorted(ids_s, [e, e + 1])
+        sel = order[lo:hi]
+        if side == "users":
+            a = np.hstack([Vm[other[sel]], np.ones((len(sel), 1))])
+            w = ratings[sel]
+        else:
+            a = Um[other[sel], :k]
+            w = ratings[sel] - Um[other[sel], k]
+        Gr = a.T @ a
+        cr = a.T @ w
+        assert np.max(np.abs(G[t] - Gr)) / max(np.max(np.abs(Gr)), 1e-30) < tol, (side, e)
+        assert np.max(np.abs(c[t] - cr)) / max(np.max(np.abs(cr)), 1.0) < tol, (side, e)
+
+
+def _first_half_step_vs_oracle(ctx, side, E, K, U0, V0, set_factors, max_it=200):
+    """The engine's first CG solve of ``side`` (reference defaults 0.01, 200)
+    against the oracle's fp64 CG (cg_least_squares restated, matrix.cpp:
+    456-529) on the GPU's own normal equations: same iteration count, final
+    rr within 1e-8 (summation order only)."""
+    from oracle import als_oracle as O
+    set_factors()
+    ctx.build_normal_equations(side)
+    G, c = ctx.normal_equations(side, np.arange(E, dtype=np.int32))
+    set_factors()
+    its, rr = ctx.half_step(side, 0.01, max_it)
+    x = (U0 if side == "users" else V0)[:E * K].astype(np.float32).copy()
+    del U0, V0
+
+    def mv(v):   # batched block GEMV, fp64 (the summation order is BLAS's)
+        return np.matmul(G, np.asarray(v, np.float64).reshape(E, K, 1)).reshape(-1)
+    ito, rro = O.cg_normal(mv, c.reshape(-1), x, 0.01, max_it)
+    print(f"{side}: engine {its} CG iterations rr {rr:.6e}, oracle {ito} rr {rro:.6e}",
+          flush=True)
+    assert its == ito, (side, its, ito)
+    assert abs(rr - rro) <= 1e-8 * abs(rro), (side, rr, rro)
+
+
+@pytest.fixture(scope="module")
+def c4():
+    """C4's data set: ML-full shape shrunk for k = 128, seeded initial factors."""
+    from movie_recommender_amd import synth
+    k = 128
+    rs = synth.movielens_like("ml-full", k)
+    assert rs.n * (k + 1) > 2 ** 30      # a size the reference's int32 indices barely hold
+    rng = np.random.default_rng(0)
+    U0 = rng.uniform(-1, 1, rs.num_users * (k + 1))
+    V0 = rng.uniform(-1, 1, rs.num_items * k)
+    return k, rs, U0, V0
+
+
+def test_c4_mlfull_k128_layout_and_gram(gpu, c4):
+    """C4 (ML-full shape at k = 128) on one GPU: both sides' device CSR and
+    Gram work lists bit-exact against their host restatement, and sampled
+    normal equations (heaviest, lightest, random entities) against fp64
+    NumPy."""
+    from movie_recommender_amd.engine import AlsContext
+    k, rs, U0, V0 = c4
+    rng = np.random.default_rng(0)
+    with AlsContext(rs.user_ids, rs.item_ids, rs.ratings, k, rs.num_users,
+                    rs.num_items) as ctx:
+        for side in ("users", "items"):
+            ids, other, E = ((rs.user_ids, rs.item_ids, rs.num_users) if side == "users"
+                             else (rs.item_ids, rs.user_ids, rs.num_items))
+            n_other = rs.num_items if side == "users" else rs.num_users
+            off, idx, val, (wb, wl, we, ws) = ctx.layout(side)
+            eoff, eidx, eval_, work = expected_layout(ids, other, rs.ratings, E,
+                                                      xcd_table_bytes=n_other * k * 4)
+            assert np.array_equal(off, eoff) and np.array_equal(idx, eidx), side
+            assert np.array_equal(val, eval_), side
+            w = np.array(work, np.int64)
+            assert np.array_equal(wb, w[:, 0]) and np.array_equal(wl, w[:, 1]), side
+            assert np.array_equal(we, w[:, 2]) and np.array_equal(ws, w[:, 3]), side
+        ctx.set_factors(U0, V0)
+        for side in ("users", "items"):
+            ids = rs.user_ids if side == "users" else rs.item_ids
+            other = rs.item_ids if side == "users" else rs.user_ids
+            cnt = np.bincount(ids)
+            ents = np.unique(np.concatenate([np.argsort(cnt)[-3:], np.argsort(cnt)[:3],
+                                             rng.integers(0, len(cnt), 6)])).astype(np.int32)
+            _sampled_gram_check(ctx, side, ids, other, rs.ratings, U0, V0, k, ents)
+
+
+@pytest.mark.parametrize("side", ["items", "users"])
+def test_c4_mlfull_k128_first_cg_vs_oracle(gpu, c4, side):
+    """C4 at full size: the first CG solve of each side (reference defaults,
+    natural stop) against the oracle's CG on the GPU's normal equations."""
+    from movie_recommender_amd.engine import AlsContext
+    k, rs, U0, V0 = c4
+    E, K = (rs.num_items, k) if side == "items" else (rs.num_users, k + 1)
+    with AlsContext(rs.user_ids, rs.item_ids, rs.ratings, k, rs.num_users,
+                    rs.num_items) as ctx:
+        _first_half_step_vs_oracle(ctx, side, E, K, U0, V0, lambda: ctx.set_factors(U0, V0))
+
+
+def test_c5_rank_slice_k128(gpu):
+    """C5 through the per-rank views of the streamed generator: the 1/8-scale
+    C5 set (1.25 M users, 125 k items, ~125 M ratings) cut into 8 cost-
+    balanced shards as bench.py does, rank 0's shard built from
+    ``user_view`` / ``item_view``; device-seeded factors equal the host
+    restatement of the hash on sampled rows of both tables (bit for bit);
+    sampled normal equations of the shard against fp64 NumPy; the shard's
+    first users CG solve moves exactly the shard's rows (the oracle-CG
+    comparison at k = 128 runs on C4 above: 156 k users x 129^2 fp64 blocks
+    would take 21 GB of host memory here)."""
+    from movie_recommender_amd import synth
+    from movie_recommender_amd.distributed import entity_cost, shard_bounds
+    from movie_recommender_amd.engine import AlsContext
+    k, world, seed = 128, 8, 7
+    gen = synth.C5Generator(scale=0.125)
+    ub = shard_bounds(entity_cost(gen.deg, k), world)
+    ib = shard_bounds(entity_cost(np.rint(gen.expected_item_counts()).astype(np.int64), k),
+                      world)
+    u0, u1, i0, i1 = int(ub[0]), int(ub[1]), int(ib[0]), int(ib[1])
+    uv = gen.user_view(u0, u1)
+    iv = gen.item_view(i0, i1)
+    assert len(uv[0]) == int(gen.deg[u0:u1].sum())
+    assert np.all((iv[1] >= i0) & (iv[1] < i1))
+    print(f"C5/8 rank 0: users [{u0},{u1}) {len(uv[0])} ratings, items [{i0},{i1}) "
+          f"{len(iv[0])} ratings", flush=True)
+    rng = np.random.default_rng(1)
+    with AlsContext(uv[0], uv[1], uv[2], k, gen.num_users, gen.num_items,
+                    user_range=(u0, u1), item_range=(i0, i1), item_view=iv) as ctx:
+        assert ctx.local_size("users") == (u0, u1 - u0, len(uv[0]))
+        assert ctx.local_size("items") == (i0, i1 - i0, len(iv[0]))
+        ctx.init_factors(seed)
+        U, V = ctx.get_factors()
+        ur = np.unique(np.concatenate([[0, u1 - 1, gen.num_users - 1],
+                                       rng.integers(0, gen.num_users, 64)]))
+        vr = np.unique(np.concatenate([[0, gen.num_items - 1], rng.integers(0, gen.num_items, 64)]))
+        assert np.array_equal(U.reshape(-1, k + 1)[ur], init_factor_rows(seed, 0, ur, k))
+        assert np.array_equal(V.reshape(-1, k)[vr], init_factor_rows(seed, 1, vr, k))
+        assert np.all(np.abs(U) < 1) and np.all(np.abs(V) < 1)
+        # sampled normal equations of the shard's users (local ids) and items
+        cnt = np.bincount(uv[0] - u0, minlength=u1 - u0)
+        ents = np.unique(np.concatenate([np.argsort(cnt)[-2:], np.argsort(cnt)[:2],
+                                         rng.integers(0, u1 - u0, 4)])).astype(np.int32)
+        _sampled_gram_check(ctx, "users", (uv[0] - u0).astype(np.int64), uv[1], uv[2], U, V, k,
+                            ents)
+        icnt = np.bincount(iv[1] - i0, minlength=i1 - i0)
+        ients = np.unique(np.concatenate([np.argsort(icnt)[-2:], np.argsort(icnt)[:2],
+                                          rng.integers(0, i1 - i0, 4)])).astype(np.int32)
+        _sampled_gram_check(ctx, "items", (iv[1] - i0).astype(np.int64), iv[0], iv[2], U, V, k,
+                            ients)
+        # the shard's first users CG solve (local: a shard context without
+        # collectives): only the shard's user rows move, V stays, rr finite
+        its, rr = ctx.half_step("users", 0.01, 8)
+        U1, V1 = ctx.get_factors()
+        print(f"C5/8 rank 0 users half-step: {its} CG iterations, rr {rr:.6e}", flush=True)
+        assert 1 <= its <= 8 and np.isfinite(rr)
+        Um, U1m = U.reshape(-1, k + 1), U1.reshape(-1, k + 1)
+        assert np.array_equal(U1m[:u0], Um[:u0]) and np.array_equal(U1m[u1:], Um[u1:])
+        assert np.array_equal(V1, V)
+        moved = np.any(U1m[u0:u1] != Um[u0:u1], axis=1)
+        assert moved.mean() > 0.99 and np.all(np.isfinite(U1m[u0:u1]))

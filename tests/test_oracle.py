@@ -126,3 +126,32 @@ def test_exact_solve_matches_numpy_lstsq():
         A = np.hstack([Vm[i[sel]], np.ones((sel.sum(), 1))])
         ref = np.linalg.lstsq(A, r[sel], rcond=None)[0]
         assert np.allclose(x[uu * 5:(uu + 1) * 5], ref, atol=1e-9)
+
+
+@pytest.mark.parametrize("name", ["als_mlshape_k10_it4.npz", "als_dense_60x50_k32_it3.npz",
+                                  "als_dense_300x200_k10.npz"])
+@pytest.mark.parametrize("tc", [1, 3])
+def test_ref_replay_bitwise_equals_reference_als(name, tc):
+    """oracle/ref_replay.als_replay (als() restated around the compiled
+    reference's own cg_least_squares_from_python) is the reference: factors
+    and ret bit-identical to als_from_python at the same thread count, so the
+    CG iteration counts it reports are the reference's (bench.py
+    cpu_baseline)."""
+    from oracle import ref
+    from oracle.ref_replay import als_replay
+    if not ref.available():
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    d = load_golden(name)
+    k = int(d["k"])
+    mi = max_iteration_of(name, d)
+    ref.set_thread_count(tc)
+    try:
+        U, V, ret = ref.als(d["user_ids"], d["item_ids"], d["ratings"], k, d["U0"], d["V0"],
+                            max_iteration=mi)
+        Ur, Vr, retr, trace = als_replay(d["user_ids"], d["item_ids"], d["ratings"], k,
+                                         d["U0"], d["V0"], max_iteration=mi)
+    finally:
+        ref.set_thread_count(1)
+    assert retr == ret
+    assert np.array_equal(Ur, U) and np.array_equal(Vr, V)
+    assert len(trace) == min(ret + 1, mi) and all(t["cg_users"] >= 1 for t in trace)
