@@ -2,7 +2,8 @@
 
 The shared library exports the reference ABI (``include/cpp_ls_lib.h``), the
 device-resident engine API (``include/mr_als.h``), the factor consumers
-(``include/mr_serving.h``), the training-set preparation
+(``include/mr_serving.h``), the general sparse least squares
+(``include/mr_cg.h``), the training-set preparation
 (``include/mr_prep.h``) and the similar-movies database
 (``include/mr_similar.h``).  There is no CPU
 fallback: if the library is missing or cannot load, every entry point raises.
@@ -52,6 +53,28 @@ ALLREDUCE_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p,
 ALLGATHER_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p,
                                 ctypes.POINTER(ctypes.c_float), ctypes.c_longlong,
                                 ctypes.POINTER(ctypes.c_longlong), ctypes.c_int)
+
+
+CG_K_NAMES = ["spmv_a", "spmv_at", "update", "setup"]
+
+
+class MrCgStats(ctypes.Structure):
+    _fields_ = [("last_iterations", ctypes.c_int),
+                ("iterations_total", ctypes.c_longlong),
+                ("solve_ms", ctypes.c_double),
+                ("kernel_ms", ctypes.c_double * len(CG_K_NAMES)),
+                ("kernel_launches", ctypes.c_longlong * len(CG_K_NAMES)),
+                ("rows", ctypes.c_longlong), ("cols", ctypes.c_longlong),
+                ("nnz", ctypes.c_longlong),
+                ("blocks_a", ctypes.c_longlong), ("blocks_at", ctypes.c_longlong)]
+
+    def as_dict(self):
+        return {"last_iterations": self.last_iterations,
+                "iterations_total": self.iterations_total, "solve_ms": self.solve_ms,
+                "kernel_ms": {n: self.kernel_ms[i] for i, n in enumerate(CG_K_NAMES)},
+                "kernel_launches": {n: self.kernel_launches[i] for i, n in enumerate(CG_K_NAMES)},
+                "rows": self.rows, "cols": self.cols, "nnz": self.nnz,
+                "blocks_a": self.blocks_a, "blocks_at": self.blocks_at}
 
 
 class MrComm(ctypes.Structure):
@@ -125,6 +148,13 @@ SIGNATURES = {
                                          ctypes.c_longlong, ctypes.c_longlong, FP, FP]),
     "mr_test_unstage_rows": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, LLP,
                                             ctypes.c_longlong, ctypes.c_int, FP, FP, FP, FP]),
+    # general sparse least squares (include/mr_cg.h)
+    "mr_cg_create": (VP, [ctypes.c_int, ctypes.c_int, ctypes.c_int, IP, IP, DP]),
+    "mr_cg_destroy": (None, [VP]),
+    "mr_cg_solve": (ctypes.c_int, [VP, DP, DP, ctypes.c_double, ctypes.c_int, DP]),
+    "mr_cg_set_timing": (ctypes.c_int, [VP, ctypes.c_int]),
+    "mr_cg_get_stats": (ctypes.c_int, [VP, ctypes.POINTER(MrCgStats)]),
+    "mr_cg_reset_stats": (ctypes.c_int, [VP]),
     # factor consumers (include/mr_serving.h)
     "mr_rec_create": (VP, [ctypes.c_int, ctypes.c_int, ctypes.c_int, DP, ctypes.c_int, IP, IP,
                            DP]),

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/cpp_ls_lib.h"
+#include "../../include/mr_cg.h"
 #include "engine.h"
 
 struct mr_als {
@@ -72,9 +73,14 @@ int cg_least_squares_from_python(int A_rows, int A_cols, int* A_row_indices,
   return guarded([&]() -> int {
     MR_CHECK(b_length == A_rows, "cg_least_squares: b_length != A_rows");
     MR_CHECK(x_length == A_cols, "cg_least_squares: x_length != A_cols");
-    return mr::cg_ls_f64(env_device(), A_rows, A_cols, A_row_indices, A_col_indices,
-                         A_values, b_values, x_values, min_r_decrease, max_iteration,
-                         final_rr);
+    // a context per call, as the reference builds its matrices per call:
+    // upload, device transpose, CG, download (include/mr_cg.h)
+    mr_cg* h = mr_cg_create(env_device(), A_rows, A_cols, A_row_indices, A_col_indices,
+                            A_values);
+    if (!h) return -1;
+    const int it = mr_cg_solve(h, b_values, x_values, min_r_decrease, max_iteration, final_rr);
+    mr_cg_destroy(h);
+    return it;
   });
 }
 

@@ -144,8 +144,11 @@ struct Engine {
   int resolve_timing();
 };
 
-int cg_ls_f64(int device, int rows, int cols, const int* rp, const int* ci,
-              const double* v, const double* b, double* x, double min_dec,
-              int max_it, double* final_rr);
+// Spin on slot target % kMirrorSlots of a host-mapped seqlock ring until the
+// state published under sequence number `target` is there (Engine::cg,
+// CgLs::solve); checks `stream` for errors / idleness, gives up after
+// timeout_s.
+int wait_published(CgMirror* ring, int target, hipStream_t stream, double timeout_s,
+                   CgMirror* out);
 
 }  // namespace mr

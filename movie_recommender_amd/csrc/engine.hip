@@ -4,7 +4,6 @@
 // Control flow follows the reference exactly:
 //   cg()         cg_least_squares        cpp/ls_lib/matrix.cpp:456-529
 //   run()        als() outer loop        cpp/ls_lib/matrix.cpp:814-892
-//   cg_ls_f64()  cg_least_squares on a general CSR A (ls_linux_dll.cpp:28-77)
 // but every numeric step runs on the GPU; the host only enqueues kernels and
 // reads the 72-byte CG state once per chunk of CG iterations.
 #include <algorithm>
@@ -575,9 +574,10 @@ int Engine::finalize_sharded(int phase, int seq) {
 // 2 target.  Checks the stream for errors and for "stream idle but nothing
 // published" (a bug), and gives up after wait_timeout_s (a stalled peer rank
 // in a sharded run).
-int Engine::wait_mirror(int target, CgMirror* out) {
+int wait_published(CgMirror* ring, int target, hipStream_t stream, double timeout_s,
+                   CgMirror* out) {
   const int want = 2 * target;
-  CgMirror* slot = h_mirror + (target & (kMirrorSlots - 1));
+  CgMirror* slot = ring + (target & (kMirrorSlots - 1));
   long spins = 0;
   const auto t0 = std::chrono::steady_clock::now();
   while (true) {
@@ -604,11 +604,15 @@ int Engine::wait_mirror(int target, CgMirror* out) {
                std::string("stream error while polling CG state: ") + hipGetErrorString(q));
       const double el =
           std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-      MR_CHECK(el < wait_timeout_s, "timed out waiting for the CG state (" +
-                                        std::to_string(el) + " s; stalled peer rank?)");
+      MR_CHECK(el < timeout_s, "timed out waiting for the CG state (" + std::to_string(el) +
+                                   " s; stalled peer rank?)");
     }
     __builtin_ia32_pause();
   }
+}
+
+int Engine::wait_mirror(int target, CgMirror* out) {
+  return wait_published(h_mirror, target, stream, wait_timeout_s, out);
 }
 
 // ----------------------------------------------------------------------------
@@ -1033,101 +1037,6 @@ int Engine::get_cg_vectors(bool user, double* r, double* p, double* q) {
     }
   }
   return 0;
-}
-
-// ----------------------------------------------------------------------------
-// General CSR CG least squares in fp64 (cg_least_squares[2]_from_python)
-// ----------------------------------------------------------------------------
-int cg_ls_f64(int device, int rows, int cols, const int* rp, const int* ci,
-              const double* v, const double* b, double* x, double min_dec,
-              int max_it, double* final_rr) {
-  MR_CHECK(rows >= 0 && cols >= 0, "negative matrix dimension");
-  MR_CHECK(rp[0] == 0 && rp[rows] >= 0, "row indices must start at 0");
-  for (int r = 0; r < rows; ++r) MR_CHECK(rp[r + 1] >= rp[r], "row indices not monotone");
-  const int64_t nnz = rp[rows];
-  for (int64_t j = 0; j < nnz; ++j)
-    MR_CHECK(ci[j] >= 0 && ci[j] < cols, "column index out of range");
-  MR_HIP(hipSetDevice(device));
-  hipStream_t s;
-  MR_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  struct Bufs {
-    hipStream_t s;
-    std::vector<void*> p;
-    ~Bufs() {
-      (void)hipStreamSynchronize(s);
-      for (void* q : p) (void)hipFree(q);
-      (void)hipStreamSynchronize(s);
-      (void)hipStreamDestroy(s);
-    }
-  } bufs{s, {}};
-  auto alloc = [&](void** q, size_t bytes) -> int {
-    MR_HIP(hipMalloc(q, bytes ? bytes : 8));   // not the stream-ordered pool (dalloc)
-    bufs.p.push_back(*q);
-    return 0;
-  };
-  int32_t *d_rp32, *d_ci, *d_rowof, *d_tidx;
-  int64_t *d_rp, *d_toff;
-  double *d_v, *d_tval, *d_b, *d_b2, *d_x, *d_r, *d_p, *d_q, *d_t, *d_part;
-  CgState *d_st, *h_st;
-  if (alloc((void**)&d_rp32, (rows + 1) * 4) || alloc((void**)&d_rp, (rows + 1) * 8) ||
-      alloc((void**)&d_ci, nnz * 4) || alloc((void**)&d_v, nnz * 8) ||
-      alloc((void**)&d_rowof, nnz * 4) || alloc((void**)&d_toff, ((int64_t)cols + 1) * 8) ||
-      alloc((void**)&d_tidx, nnz * 4) || alloc((void**)&d_tval, nnz * 8) ||
-      alloc((void**)&d_b, (int64_t)rows * 8) || alloc((void**)&d_b2, (int64_t)cols * 8) ||
-      alloc((void**)&d_x, (int64_t)cols * 8) || alloc((void**)&d_r, (int64_t)cols * 8) ||
-      alloc((void**)&d_p, (int64_t)cols * 8) || alloc((void**)&d_q, (int64_t)cols * 8) ||
-      alloc((void**)&d_t, (int64_t)rows * 8) || alloc((void**)&d_part, kUpdParts * 8) ||
-      alloc((void**)&d_st, sizeof(CgState)))
-    return -1;
-  MR_HIP(hipHostMalloc((void**)&h_st, sizeof(CgState), hipHostMallocDefault));
-  struct HFree { CgState* h; ~HFree() { (void)hipHostFree(h); } } hf{h_st};
-  MR_H2D(d_rp32, rp, (rows + 1) * 4, s);
-  if (nnz) {
-    MR_H2D(d_ci, ci, nnz * 4, s);
-    MR_H2D(d_v, v, nnz * 8, s);
-  }
-  if (rows) MR_H2D(d_b, b, (int64_t)rows * 8, s);
-  if (cols) MR_H2D(d_x, x, (int64_t)cols * 8, s);
-  if (launch_i32_to_i64(s, rows + 1, d_rp32, d_rp)) return -1;
-  // explicit transpose on the device (sparse_matrix_transpose, matrix.cpp:617-692)
-  if (launch_rows_of(s, rows, d_rp, d_rowof)) return -1;
-  if (build_csr<double, double>(s, nnz, cols, d_ci, 0, d_rowof, d_v, d_toff, d_tidx, d_tval))
-    return -1;
-  // b2 = A^T b
-  if (launch_spmv_f64(s, cols, d_toff, d_tidx, d_tval, d_b, d_b2)) return -1;
-  memset(h_st, 0, sizeof(CgState));
-  h_st->min_dec = min_dec;
-  h_st->max_it = max_it;
-  MR_HIP(hipMemcpyAsync(d_st, h_st, sizeof(CgState), hipMemcpyHostToDevice, s));
-  // r0 = A^T A x - b2, p0 = -r0
-  if (launch_spmv_f64(s, rows, d_rp, d_ci, d_v, d_x, d_t)) return -1;
-  if (launch_spmv_f64(s, cols, d_toff, d_tidx, d_tval, d_t, d_q)) return -1;
-  if (launch_update_f64(s, d_st, UPD_INIT, cols, d_x, d_r, d_p, d_q, d_b2, d_part, kUpdParts))
-    return -1;
-  if (launch_cg_control(s, d_st, CG_INIT, CTL_BOTH, d_part, kUpdParts)) return -1;
-  int t = 0, chunk_it = 4;
-  while (true) {
-    for (int c = 0; c < chunk_it; ++c, ++t) {
-      if (t > 0 && launch_p_update_f64(s, d_st, cols, d_p, d_r)) return -1;
-      if (launch_spmv_f64(s, rows, d_rp, d_ci, d_v, d_p, d_t)) return -1;
-      if (launch_spmv_f64(s, cols, d_toff, d_tidx, d_tval, d_t, d_q)) return -1;
-      if (launch_dot_f64(s, d_st, cols, d_p, d_q, d_part, kUpdParts)) return -1;
-      if (launch_cg_control(s, d_st, CG_ALPHA, CTL_BOTH, d_part, kUpdParts)) return -1;
-      if (launch_update_f64(s, d_st, UPD_STEP, cols, d_x, d_r, d_p, d_q, d_b2, d_part,
-                            kUpdParts))
-        return -1;
-      if (launch_cg_control(s, d_st, CG_BETA, CTL_BOTH, d_part, kUpdParts)) return -1;
-    }
-    MR_HIP(hipMemcpyAsync(h_st, d_st, sizeof(CgState), hipMemcpyDeviceToHost, s));
-    MR_HIP(hipStreamSynchronize(s));
-    if (h_st->done) break;
-    MR_CHECK(t <= max_it + 64, "CG did not terminate");
-    chunk_it = std::min(chunk_it * 2, 16);
-  }
-  if (cols) MR_D2H(x, d_x, (int64_t)cols * 8, s);
-  MR_HIP(hipStreamSynchronize(s));
-  if (final_rr) *final_rr = h_st->final_rr;
-  return h_st->ret;
 }
 
 }  // namespace mr

@@ -2405,56 +2405,129 @@ int launch_predict(hipStream_t s, int64_t n, int k, int ldk, const int* uid,
 }
 
 // ---------------------------------------------------------------------------
-// General CSR least squares in fp64 (cg_least_squares_from_python path):
-// SpMV with 16 lanes per row, dot / update partials with a fixed grid.
+// General CSR least squares in fp64 (cg_least_squares_from_python,
+// matrix.cpp:456-529): three kernels per CG iteration on A (CSR) and its
+// explicit transpose At (CSR of A^T, built once per context):
+//   K1  t = A p           rows of A; p = -r + beta p formed at each gather
+//                         (matrix.cpp:521 of the previous iteration)
+//   K2  q = At t          rows of At = columns of A; each writes its new p_j
+//                         and adds p_j q_j to the p.Ap partial; the last
+//                         workgroup computes alpha (:497)
+//   K3  x += alpha p, r += alpha q, r.r partial; the last workgroup applies
+//       the BETA rule and publishes the state (:501-518)
+// K1 / K2 are CSR-stream SpMVs: a workgroup takes a "row block" (consecutive
+// rows holding <= SP_TILE non-zeros, <= 256 rows; a longer row is a block of
+// its own), streams the block's values / column ids with consecutive lanes
+// on consecutive non-zeros (fully coalesced), stages the products in LDS,
+// then sums each row from LDS with a group of G threads (G = the largest
+// power of two <= 256 / rows; G = 1: one thread per row in index order, the
+// reference's own row order).  Row blocks are dealt to a fixed grid
+// (grid-stride), so every partial sum has a fixed order: results are
+// reproducible.  Arithmetic follows the reference's expressions with
+// contraction off (x86 -O2 builds do not fuse): -1*r + beta*p, x + alpha*p,
+// r + alpha*q, sum += v*x.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void spmv_f64_kernel(
-    int64_t rows, const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
-    const double* __restrict__ v, const double* __restrict__ x, double* __restrict__ y) {
-  const int sub = threadIdx.x & 15;
-  for (int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4; row < rows;
-       row += ((int64_t)gridDim.x * blockDim.x) >> 4) {
-    double s = 0.0;
-    for (int64_t j = rp[row] + sub; j < rp[row + 1]; j += 16) s += v[j] * x[ci[j]];
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 16);
-    if (sub == 0) y[row] = s;
+constexpr int SP_THREADS = 256;
+constexpr int SP_TILE = kSpTile;     // staged products per row block (16 KiB fp64)
+
+template <int GATHER, int OUT>
+__global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
+    const CgState* __restrict__ st, int64_t n_blk, const int64_t* __restrict__ blk,
+    const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
+    const double* __restrict__ v, const double* __restrict__ xa, const double* __restrict__ xb,
+    double* __restrict__ out, double* __restrict__ pv, const double* __restrict__ rv,
+    int update_p, double* __restrict__ partials, CgState* fst) {
+#pragma clang fp contract(off)
+  if (st && ald(&st->done)) return;
+  const double beta = (st && (GATHER == SPG_P || update_p)) ? ald(&st->beta) : 0.0;
+  __shared__ double prod[SP_TILE];
+  __shared__ double sh[SP_THREADS / 64];
+  const int t = threadIdx.x;
+  double d = 0.0;   // OUT == SPO_CG: this thread's share of p.q
+  auto gather = [&](int32_t c) -> double {
+    if constexpr (GATHER == SPG_P) return -1.0 * xa[c] + beta * xb[c];
+    else return xa[c];
+  };
+  auto emit = [&](int64_t row, double s) {
+    out[row] = s;
+    if constexpr (OUT == SPO_CG) {
+      double pn = pv[row];
+      if (update_p) {
+        pn = -1.0 * rv[row] + beta * pn;   // vect_add(-1, r, beta, p, p)
+        pv[row] = pn;
+      }
+      d += pn * s;
+    }
+  };
+  for (int64_t b = blockIdx.x; b < n_blk; b += gridDim.x) {
+    const int64_t r0 = blk[b], r1 = blk[b + 1];
+    const int64_t n0 = rp[r0], n1 = rp[r1];
+    if (n1 - n0 <= SP_TILE) {
+      for (int64_t j = n0 + t; j < n1; j += SP_THREADS) prod[j - n0] = v[j] * gather(ci[j]);
+      __syncthreads();
+      const int R = (int)(r1 - r0);
+      int G = 1;
+      while (G < 64 && 2 * G * R <= SP_THREADS) G *= 2;
+      const int lr = t / G, g = t & (G - 1);
+      double s = 0.0;
+      if (lr < R) {
+        const int64_t e = rp[r0 + lr + 1] - n0;
+        for (int64_t j = rp[r0 + lr] - n0 + g; j < e; j += G) s += prod[j];
+      }
+      for (int o = G / 2; o > 0; o >>= 1) s += __shfl_xor(s, o);
+      if (lr < R && g == 0) emit(r0 + lr, s);
+      __syncthreads();   // prod is reused by the next block
+    } else {             // one long row: per-thread strided sums, fixed-order tree
+      double s = 0.0;
+      for (int64_t j = n0 + t; j < n1; j += SP_THREADS) s += v[j] * gather(ci[j]);
+      s = block_sum_f64<SP_THREADS>(s, sh);
+      if (t == 0) emit(r0, s);
+      __syncthreads();
+    }
+  }
+  if constexpr (OUT == SPO_CG) {
+    const double tot = block_sum_f64<SP_THREADS>(d, sh);
+    if (fst) {
+      store_partial(partials, tot);
+      last_block_finalize(fst, CG_ALPHA, partials, nullptr, 0, sh);
+    } else if (t == 0) {
+      partials[blockIdx.x] = tot;
+    }
   }
 }
 
-int launch_spmv_f64(hipStream_t s, int64_t rows, const int64_t* rp,
-                    const int32_t* ci, const double* v, const double* x, double* y) {
-  if (rows <= 0) return 0;
-  spmv_f64_kernel<<<grid_for(rows * 16), 256, 0, s>>>(rows, rp, ci, v, x, y);
+int launch_csr_spmv(hipStream_t s, int gather, int out_mode, const CgState* st, int64_t n_blk,
+                    const int64_t* blk, const int64_t* rp, const int32_t* ci, const double* v,
+                    const double* xa, const double* xb, double* out, double* pv,
+                    const double* rv, int update_p, double* partials, int n_part,
+                    CgState* fst) {
+  if (n_blk <= 0) return 0;
+  const dim3 grid((unsigned)std::min<int64_t>(n_blk, n_part));
+#define MR_SP(GA, OU)                                                                      \
+  MR_LAUNCH((csr_spmv_kernel<GA, OU>), grid, dim3(SP_THREADS), 0, s, st, n_blk, blk, rp, ci, \
+            v, xa, xb, out, pv, rv, update_p, partials, fst)
+  if (out_mode == SPO_CG) {
+    if (gather == SPG_P) MR_SP(SPG_P, SPO_CG);
+    else MR_SP(SPG_X, SPO_CG);
+  } else {
+    if (gather == SPG_P) MR_SP(SPG_P, SPO_STORE);
+    else MR_SP(SPG_X, SPO_STORE);
+  }
+#undef MR_SP
   MR_HIP(hipGetLastError());
   return 0;
 }
 
-__global__ __launch_bounds__(256) void dot_f64_kernel(const CgState* st, int64_t n,
-                                                      const double* __restrict__ a,
-                                                      const double* __restrict__ b,
-                                                      double* __restrict__ partials) {
-  if (st && ald(&st->done)) return;
-  __shared__ double sh[4];
-  double acc = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x)
-    acc += a[i] * b[i];
-  const double tot = block_sum_f64<256>(acc, sh);
-  if (threadIdx.x == 0) partials[blockIdx.x] = tot;
-}
-
-int launch_dot_f64(hipStream_t s, const CgState* st, int64_t n, const double* a,
-                   const double* b, double* partials, int n_part) {
-  dot_f64_kernel<<<dim3(n_part), 256, 0, s>>>(st, n, a, b, partials);
-  MR_HIP(hipGetLastError());
-  return 0;
-}
-
-__global__ __launch_bounds__(256) void update_f64_kernel(
+// K3 (and the INIT update): x += alpha p, r += alpha q (vect_add(1, x, alpha,
+// p, x), matrix.cpp:501-503) / r0 = q - b2, p0 = -r0 (:468-476); r.r partials
+// (:507 / :485) in a fixed grid; the last workgroup applies the INIT / BETA
+// rule and publishes the state.
+__global__ __launch_bounds__(256) void cgls_update_kernel(
     const CgState* __restrict__ st, int mode, int64_t n, double* __restrict__ x,
     double* __restrict__ r, double* __restrict__ p, const double* __restrict__ q,
-    const double* __restrict__ c, double* __restrict__ partials) {
+    const double* __restrict__ b2, double* __restrict__ partials, CgState* fst,
+    CgMirror* mirror, int seq) {
+#pragma clang fp contract(off)
   if (ald(&st->done)) return;
   __shared__ double sh[4];
   const double alpha = ald(&st->alpha);
@@ -2463,40 +2536,25 @@ __global__ __launch_bounds__(256) void update_f64_kernel(
        i += (int64_t)gridDim.x * blockDim.x) {
     double rv;
     if (mode == UPD_INIT) {
-      rv = q[i] - c[i];
-      p[i] = -rv;
+      rv = 1.0 * q[i] + -1.0 * b2[i];
+      p[i] = -1.0 * rv;
     } else {
-      x[i] = x[i] + alpha * p[i];
-      rv = r[i] + alpha * q[i];
+      x[i] = 1.0 * x[i] + alpha * p[i];
+      rv = 1.0 * r[i] + alpha * q[i];
     }
     r[i] = rv;
     acc += rv * rv;
   }
   const double tot = block_sum_f64<256>(acc, sh);
-  if (threadIdx.x == 0) partials[blockIdx.x] = tot;
+  store_partial(partials, tot);
+  last_block_finalize(fst, mode == UPD_INIT ? CG_INIT : CG_BETA, partials, mirror, seq, sh);
 }
 
-int launch_update_f64(hipStream_t s, const CgState* st, int mode, int64_t n,
-                      double* x, double* r, double* p, const double* q,
-                      const double* c, double* partials, int n_part) {
-  update_f64_kernel<<<dim3(n_part), 256, 0, s>>>(st, mode, n, x, r, p, q, c, partials);
-  MR_HIP(hipGetLastError());
-  return 0;
-}
-
-__global__ void p_update_f64_kernel(const CgState* __restrict__ st, int64_t n,
-                                    double* __restrict__ p, const double* __restrict__ r) {
-  if (ald(&st->done)) return;
-  const double beta = ald(&st->beta);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x)
-    p[i] = -r[i] + beta * p[i];
-}
-
-int launch_p_update_f64(hipStream_t s, const CgState* st, int64_t n, double* p,
-                        const double* r) {
-  if (n <= 0) return 0;
-  p_update_f64_kernel<<<grid_for(n), 256, 0, s>>>(st, n, p, r);
+int launch_cgls_update(hipStream_t s, const CgState* st, int mode, int64_t n, double* x,
+                       double* r, double* p, const double* q, const double* b2,
+                       double* partials, int n_part, CgState* fst, CgMirror* mirror, int seq) {
+  MR_LAUNCH(cgls_update_kernel, dim3(n_part), dim3(256), 0, s, st, mode, n, x, r, p, q, b2,
+            partials, fst, mirror, seq);
   MR_HIP(hipGetLastError());
   return 0;
 }

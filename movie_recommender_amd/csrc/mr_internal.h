@@ -279,17 +279,25 @@ int launch_init_factors(hipStream_t s, int64_t rows, int k, int ldk, uint64_t se
 int launch_predict(hipStream_t s, int64_t n, int k, int ldk, const int* uid,
                    const int* iid, const float* Ufac, const float* Ubias,
                    const float* Vfac, double* out);
-// General CSR (fp64) CG least squares pieces.
-int launch_spmv_f64(hipStream_t s, int64_t rows, const int64_t* rp,
-                    const int32_t* ci, const double* v, const double* x,
-                    double* y);
-int launch_dot_f64(hipStream_t s, const CgState* st, int64_t n, const double* a,
-                   const double* b, double* partials, int n_part);
-int launch_update_f64(hipStream_t s, const CgState* st, int mode, int64_t n,
-                      double* x, double* r, double* p, const double* q,
-                      const double* c, double* partials, int n_part);
-int launch_p_update_f64(hipStream_t s, const CgState* st, int64_t n,
-                        double* p, const double* r);
+// General CSR (fp64) CG least squares (cg_least_squares_from_python):
+// CSR-stream SpMV over row blocks blk[0..n_blk] (consecutive rows with
+// <= 2048 non-zeros, <= 256 rows, or one longer row), fixed grid of
+// min(n_blk, n_part) workgroups.  gather SPG_X: x_c = xa[c]; SPG_P: p_c =
+// -xa[c] + beta xb[c] (xa = r, xb = p).  out SPO_STORE: out[row] = sum;
+// SPO_CG: out[row] = q_row, p_row updated in pv (update_p) and p.q summed,
+// the last workgroup computes alpha (fst, partials[n_part]).
+enum SpGather { SPG_X = 0, SPG_P = 1 };
+enum SpOut { SPO_STORE = 0, SPO_CG = 1 };
+constexpr int kSpTile = 2048;
+constexpr int kSpMaxRows = 256;
+int launch_csr_spmv(hipStream_t s, int gather, int out_mode, const CgState* st, int64_t n_blk,
+                    const int64_t* blk, const int64_t* rp, const int32_t* ci, const double* v,
+                    const double* xa, const double* xb, double* out, double* pv,
+                    const double* rv, int update_p, double* partials, int n_part,
+                    CgState* fst);
+int launch_cgls_update(hipStream_t s, const CgState* st, int mode, int64_t n, double* x,
+                       double* r, double* p, const double* q, const double* b2,
+                       double* partials, int n_part, CgState* fst, CgMirror* mirror, int seq);
 int launch_rows_of(hipStream_t s, int64_t rows, const int64_t* rp,
                    int32_t* row_of);
 int launch_i32_to_i64(hipStream_t s, int64_t n, const int32_t* in, int64_t* out);

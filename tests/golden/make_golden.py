@@ -381,6 +381,67 @@ def g9():
           "agreement", ag.min(), ag.max())
 
 
+def bench_matrix(rows, cols, per_row, seed):
+    """The reference's least-squares benchmark matrix
+    (``cpp/ls/main.cpp:838-905``, ``fill_matrix_with_sparse_random_data``):
+    every row holds ``per_row`` consecutive columns starting at a uniform
+    column in [0, cols - per_row], values uniform(-10, 10); b uniform(-10,
+    10) (``vect_rand``), x starts at 0 (``ColVector x(cols)``)."""
+    rng = np.random.default_rng(seed)
+    start = rng.integers(0, cols - per_row + 1, rows)
+    ci = (start[:, None] + np.arange(per_row)).astype(np.int32).reshape(-1)
+    rp = (np.arange(rows + 1, dtype=np.int64) * per_row).astype(np.int32)
+    v = rng.uniform(-10, 10, rows * per_row)
+    b = rng.uniform(-10, 10, rows)
+    return rp, ci, v, b, np.zeros(cols)
+
+
+def g10():
+    """Round 3: general CG least squares (cg_least_squares_from_python) on
+    the structures the CSR-stream kernels distinguish: the reference's own
+    benchmark matrix (10 consecutive non-zeros per row, main.cpp:760-798) at
+    20,000 x 2,000; and a matrix with rows longer than the 2,048-non-zero
+    stage tile, columns referenced by more than 2,048 rows, empty rows and
+    empty columns.  Reference at thread counts 8 and 1 (spread recorded)."""
+    cases = {}
+    rp, ci, v, b, x0 = bench_matrix(20_000, 2_000, 10, 31)
+    cases["cg_bench_20000x2000.npz"] = (rp, ci, v, b, x0, 2_000)
+    rng = np.random.default_rng(32)
+    rows, cols = 6_000, 2_500
+    dens = np.full(rows, 0.004)
+    dens[[5, 77, 2500]] = [0.9, 0.99, 0.85]      # rows of ~2.2 k, 2.5 k, 2.1 k non-zeros
+    dens[[10, 11, 3000]] = 0.0                   # empty rows
+    A = (rng.random((rows, cols)) < dens[:, None]) * rng.uniform(-1, 1, (rows, cols))
+    A[:, [3, 4, 2000]] = 0.0                     # empty columns
+    A[:, 17] = rng.uniform(-1, 1, rows)          # A^T row 17: 6,000 non-zeros
+    A /= np.sqrt(np.maximum(1.0, np.count_nonzero(A, axis=1) / 10.0))[:, None]   # comparable row norms
+    rp, ci, v = dense_csr(A)
+    b = rng.normal(0, 1, rows)
+    x0 = rng.uniform(-1, 1, cols)
+    cases["cg_longrows_6000x2500.npz"] = (rp, ci, v, b, x0, cols)
+    # a column referenced by > 2,048 rows: tall, thin, one dense column
+    rows, cols = 5_000, 300
+    A = (rng.random((rows, cols)) < 0.01) * rng.uniform(-1, 1, (rows, cols))
+    A[:, 7] = rng.uniform(-1, 1, rows)           # A^T row 7: 5,000 non-zeros
+    rp, ci, v = dense_csr(A)
+    b = rng.normal(0, 1, rows)
+    x0 = np.zeros(cols)
+    cases["cg_tallcol_5000x300.npz"] = (rp, ci, v, b, x0, cols)
+    for name, (rp, ci, v, b, x0, nc) in cases.items():
+        res = {}
+        for tc in (8, 1):
+            ref.set_thread_count(tc)
+            res[tc] = ref.cg_least_squares(rp, ci, v, nc, b, x0)
+        x, it, rr = res[8]
+        spread = float(np.max(np.abs(res[1][0] - x)) / max(np.max(np.abs(x)), 1e-300))
+        np.savez_compressed(os.path.join(HERE, name), row_ptr=rp, col_idx=ci, vals=v, ncols=nc,
+                            b=b, x0=x0, x=x, iterations=it, final_rr=rr,
+                            iterations_tc1=res[1][1], tc_spread=spread, meta=json.dumps(_meta(8)))
+        print("G10", name, "nnz", len(v), "it", it, "tc1 it", res[1][1], "rr", rr,
+              "spread", spread, flush=True)
+    ref.set_thread_count(1)
+
+
 if __name__ == "__main__":
     steps = sys.argv[1:] or ["g1", "g2", "g3", "g4", "g5", "g6", "g7", "g8"]
     for s in steps:

@@ -1,0 +1,114 @@
+"""General sparse least squares on the GPU (``cg_least_squares_from_python``,
+``cpp/ls_lib/ls_linux_dll.cpp:28-77`` -> ``matrix.cpp:456-529``): the
+CSR-stream SpMV kernels and the fused CG update, through the reference ABI
+and the device-resident context (``include/mr_cg.h``), against golden
+vectors of the compiled reference (``tests/golden/make_golden.py`` g1, g5,
+g10) and the oracle's restatement."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import load_golden, rel_err
+from oracle import als_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+GOLDENS = ["cg_dense_200x50.npz", "cg_edge_sparse.npz", "cg_bench_20000x2000.npz",
+           "cg_longrows_6000x2500.npz", "cg_tallcol_5000x300.npz"]
+
+
+def _abi(fn, d, x0=None, min_dec=0.01, max_it=200):
+    from movie_recommender_amd import _lib
+    rp = np.ascontiguousarray(d["row_ptr"], np.int32)
+    ci = np.ascontiguousarray(d["col_idx"], np.int32)
+    v = np.ascontiguousarray(d["vals"], np.float64)
+    b = np.ascontiguousarray(d["b"], np.float64)
+    x = np.array(d["x0"] if x0 is None else x0, np.float64)
+    rr = ctypes.c_double(0)
+    it = fn(len(rp) - 1, int(d["ncols"]), rp.ctypes.data_as(_lib.IP), ci.ctypes.data_as(_lib.IP),
+            v.ctypes.data_as(_lib.DP), len(b), b.ctypes.data_as(_lib.DP), len(x),
+            x.ctypes.data_as(_lib.DP), float(min_dec), int(max_it), ctypes.byref(rr))
+    assert it >= 0, _lib.last_error()
+    return x, it, rr.value
+
+
+@pytest.mark.parametrize("name", GOLDENS)
+def test_cg_goldens_through_reference_abi(gpu, name):
+    """Both reference symbols: same iteration count as the compiled reference,
+    x within max(1e-9, 20 x the reference's own thread-count spread), final
+    rr within 1e-6 relative."""
+    d = load_golden(name)
+    tol = max(1e-9, 20 * float(d["tc_spread"])) if "tc_spread" in d else 1e-9
+    for fn in (gpu.cg_least_squares_from_python, gpu.cg_least_squares2_from_python):
+        x, it, rr = _abi(fn, d)
+        assert it == int(d["iterations"]), (name, it, int(d["iterations"]))
+        assert rel_err(x, d["x"]) <= tol, (name, rel_err(x, d["x"]))
+        assert abs(rr - float(d["final_rr"])) <= 1e-6 * max(1.0, float(d["final_rr"]))
+
+
+@pytest.mark.parametrize("max_it", [0, 1, 2, 3, 7])
+@pytest.mark.parametrize("min_dec", [0.01, 0.3])
+def test_cg_stop_rules_vs_oracle(gpu, max_it, min_dec):
+    """max_iteration and min_r_decrease (the two-strikes stagnation rule) on
+    the benchmark-structure matrix against the oracle's restatement."""
+    d = load_golden("cg_bench_20000x2000.npz")
+    x, it, rr = _abi(gpu.cg_least_squares_from_python, d, min_dec=min_dec, max_it=max_it)
+    xo, ito, rro = O.cg_least_squares(d["row_ptr"], d["col_idx"], d["vals"], int(d["ncols"]),
+                                      d["b"], d["x0"], min_dec, max_it)
+    assert it == ito
+    assert rel_err(x, xo) <= 1e-10 if max_it else np.array_equal(x, d["x0"])
+    assert abs(rr - rro) <= 1e-9 * max(1.0, rro)
+
+
+def test_cg_context_reuse_and_stats(gpu):
+    """One device context, several right-hand sides and starts: each solve
+    equals a fresh reference-ABI call; the kernel timing classes fill in."""
+    from movie_recommender_amd import _lib
+    L = _lib.lib()
+    d = load_golden("cg_bench_20000x2000.npz")
+    rp = np.ascontiguousarray(d["row_ptr"], np.int32)
+    ci = np.ascontiguousarray(d["col_idx"], np.int32)
+    v = np.ascontiguousarray(d["vals"], np.float64)
+    h = L.mr_cg_create(0, len(rp) - 1, int(d["ncols"]), rp.ctypes.data_as(_lib.IP),
+                       ci.ctypes.data_as(_lib.IP), v.ctypes.data_as(_lib.DP))
+    assert h, _lib.last_error()
+    try:
+        _lib.check(L.mr_cg_set_timing(h, 1), "mr_cg_set_timing")
+        rng = np.random.default_rng(3)
+        total = 0
+        for trial in range(3):
+            b = d["b"] if trial == 0 else rng.uniform(-10, 10, len(d["b"]))
+            x0 = d["x0"] if trial < 2 else rng.uniform(-1, 1, int(d["ncols"]))
+            x = np.array(x0, np.float64)
+            rr = ctypes.c_double(0)
+            it = L.mr_cg_solve(h, np.ascontiguousarray(b).ctypes.data_as(_lib.DP),
+                               x.ctypes.data_as(_lib.DP), 0.01, 200, ctypes.byref(rr))
+            assert it > 0, _lib.last_error()
+            total += it
+            xr, itr, rrr = _abi(gpu.cg_least_squares_from_python, dict(d, b=b), x0=x0)
+            assert it == itr and np.array_equal(x, xr) and rr.value == rrr
+        st = _lib.MrCgStats()
+        _lib.check(L.mr_cg_get_stats(h, ctypes.byref(st)), "mr_cg_get_stats")
+        s = st.as_dict()
+        assert s["iterations_total"] == total and s["nnz"] == len(v)
+        assert s["kernel_launches"]["spmv_a"] == total
+        assert s["kernel_launches"]["spmv_at"] == total and s["kernel_launches"]["update"] == total
+        assert s["kernel_launches"]["setup"] == 3 and s["solve_ms"] > 0
+        assert s["blocks_a"] == -(-(len(rp) - 1) // 204)   # 10 nnz/row: 204 rows per block
+    finally:
+        L.mr_cg_destroy(h)
+
+
+def test_cg_rejects_bad_input(gpu):
+    from movie_recommender_amd import _lib
+    L = _lib.lib()
+    rp = np.array([0, 2, 3], np.int32)
+    ci = np.array([0, 5, 1], np.int32)      # column 5 outside 3 columns
+    v = np.ones(3)
+    assert not L.mr_cg_create(0, 2, 3, rp.ctypes.data_as(_lib.IP), ci.ctypes.data_as(_lib.IP),
+                              v.ctypes.data_as(_lib.DP))
+    rp = np.array([0, 2, 1], np.int32)      # not monotone
+    ci = np.array([0, 1, 1], np.int32)
+    assert not L.mr_cg_create(0, 2, 3, rp.ctypes.data_as(_lib.IP), ci.ctypes.data_as(_lib.IP),
+                              v.ctypes.data_as(_lib.DP))

@@ -155,3 +155,16 @@ def test_ref_replay_bitwise_equals_reference_als(name, tc):
     assert retr == ret
     assert np.array_equal(Ur, U) and np.array_equal(Vr, V)
     assert len(trace) == min(ret + 1, mi) and all(t["cg_users"] >= 1 for t in trace)
+
+
+@pytest.mark.parametrize("name", ["cg_bench_20000x2000.npz", "cg_longrows_6000x2500.npz",
+                                  "cg_tallcol_5000x300.npz"])
+def test_cg_goldens_round3(name):
+    """The restatement on the general-CG goldens of round 3 (benchmark
+    structure, rows / columns longer than the GPU's stage tile)."""
+    d = load_golden(name)
+    x, it, rr = O.cg_least_squares(d["row_ptr"], d["col_idx"], d["vals"], int(d["ncols"]),
+                                   d["b"], d["x0"])
+    assert it == int(d["iterations"])
+    assert rel_err(x, d["x"]) < max(1e-10, 20 * float(d["tc_spread"]))
+    assert abs(rr - float(d["final_rr"])) <= 1e-8 * max(1.0, float(d["final_rr"]))
