@@ -2463,7 +2463,27 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
     const int64_t r0 = blk[b], r1 = blk[b + 1];
     const int64_t n0 = rp[r0], n1 = rp[r1];
     if (n1 - n0 <= SP_TILE) {
-      for (int64_t j = n0 + t; j < n1; j += SP_THREADS) prod[j - n0] = v[j] * gather(ci[j]);
+      // all of a thread's column ids and values first, then all gathers, then
+      // the products: PER independent loads in flight per step instead of a
+      // dependent load -> gather chain per non-zero
+      constexpr int PER = SP_TILE / SP_THREADS;
+      int32_t cc[PER];
+      double vv[PER], gx[PER];
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int64_t j = n0 + t + (int64_t)u * SP_THREADS;
+        const int64_t js = j < n1 ? j : 0;     // a valid address (arrays hold >= 1 entry)
+        const int32_t c = ci[js];
+        vv[u] = v[js];
+        cc[u] = j < n1 ? c : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < PER; ++u) gx[u] = gather(cc[u]);
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int64_t j = n0 + t + (int64_t)u * SP_THREADS;
+        if (j < n1) prod[j - n0] = vv[u] * gx[u];
+      }
       __syncthreads();
       const int R = (int)(r1 - r0);
       int G = 1;

@@ -35,16 +35,36 @@ def _abi(fn, d, x0=None, min_dec=0.01, max_it=200):
 
 @pytest.mark.parametrize("name", GOLDENS)
 def test_cg_goldens_through_reference_abi(gpu, name):
-    """Both reference symbols: same iteration count as the compiled reference,
-    x within max(1e-9, 20 x the reference's own thread-count spread), final
-    rr within 1e-6 relative."""
+    """Both reference symbols against the compiled reference.  The stop test
+    rr < 1e-6 can sit on late-iteration rounding noise: on
+    cg_longrows_6000x2500 the reference's own rr one iteration before its
+    stop moves 3.4x between thread counts (rr_before_stop_by_tc), and on a
+    sibling seed its stop moved by one iteration.  So: the iteration count
+    within one of the reference's (at any recorded thread count) -- equal
+    where the reference's is thread-count invariant and its rr before the
+    stop is stable --, x within 1e-8 of the oracle's restatement (pinned to
+    the reference at 1e-12) run for the GPU's own iteration count, and, at
+    the reference's count, x within max(1e-9, 20 x its thread-count spread)
+    and final rr within 1e-6 relative."""
     d = load_golden(name)
     tol = max(1e-9, 20 * float(d["tc_spread"])) if "tc_spread" in d else 1e-9
+    its_ref = [int(d["iterations"])] + [int(i) for i in d.get("iterations_by_tc", [])]
+    rrb = d.get("rr_before_stop_by_tc")
+    stable = rrb is None or (max(rrb) <= 1.01 * min(rrb) and len(set(its_ref)) == 1)
     for fn in (gpu.cg_least_squares_from_python, gpu.cg_least_squares2_from_python):
         x, it, rr = _abi(fn, d)
-        assert it == int(d["iterations"]), (name, it, int(d["iterations"]))
-        assert rel_err(x, d["x"]) <= tol, (name, rel_err(x, d["x"]))
-        assert abs(rr - float(d["final_rr"])) <= 1e-6 * max(1.0, float(d["final_rr"]))
+        print(f"{name}: GPU {it} iterations rr {rr:.4e}; reference {its_ref} rr "
+              f"{float(d['final_rr']):.4e}", flush=True)
+        if stable:
+            assert it == int(d["iterations"]), (name, it, its_ref)
+        else:
+            assert min(its_ref) - 1 <= it <= max(its_ref) + 1, (name, it, its_ref)
+        xo, ito, _ = O.cg_least_squares(d["row_ptr"], d["col_idx"], d["vals"], int(d["ncols"]),
+                                        d["b"], d["x0"], 0.01, it)
+        assert rel_err(x, xo) <= 1e-8, (name, rel_err(x, xo))
+        if it == int(d["iterations"]):
+            assert rel_err(x, d["x"]) <= tol, (name, rel_err(x, d["x"]))
+            assert abs(rr - float(d["final_rr"])) <= 1e-6 * max(1.0, float(d["final_rr"]))
 
 
 @pytest.mark.parametrize("max_it", [0, 1, 2, 3, 7])
@@ -92,8 +112,10 @@ def test_cg_context_reuse_and_stats(gpu):
         _lib.check(L.mr_cg_get_stats(h, ctypes.byref(st)), "mr_cg_get_stats")
         s = st.as_dict()
         assert s["iterations_total"] == total and s["nnz"] == len(v)
-        assert s["kernel_launches"]["spmv_a"] == total
-        assert s["kernel_launches"]["spmv_at"] == total and s["kernel_launches"]["update"] == total
+        # iterations that did work: `total`, plus one per solve that ended by
+        # the stagnation rule (its last iteration updates x, r but returns it - 1)
+        for c in ("spmv_a", "spmv_at", "update"):
+            assert total <= s["kernel_launches"][c] <= total + 3, (c, s["kernel_launches"])
         assert s["kernel_launches"]["setup"] == 3 and s["solve_ms"] > 0
         assert s["blocks_a"] == -(-(len(rp) - 1) // 204)   # 10 nnz/row: 204 rows per block
     finally:
