@@ -114,6 +114,19 @@ int mr_rccl_unique_id(unsigned char out[128]);
 int mr_als_set_rccl(mr_als* ctx, const unsigned char id[128], int rank, int world,
                     const long long* user_begin, const long long* item_begin);
 
+/* Peer all-reduce of the CG scalars (sharded runs, any transport): instead
+ * of an all-reduce launch per scalar, the thread that finalizes each CG
+ * reduction writes its sum into every rank's exchange buffer (IPC-mapped
+ * device memory; over xGMI between GPUs), waits for all ranks' records and
+ * sums them in rank order -- identical bits on every rank, and the CG then
+ * runs the single-GPU launch sequence (2 kernels per iteration).  Each rank:
+ * mr_als_peer_handle (64 bytes), exchange them (rank order), then
+ * mr_als_set_peer with the world x 64 bytes.  Reference scalars:
+ * matrix.cpp:485, 497, 507.  A peer that does not arrive within ~30 s fails
+ * the solve (< 0) instead of hanging. */
+int mr_als_peer_handle(mr_als* ctx, unsigned char out[64]);
+int mr_als_set_peer(mr_als* ctx, const unsigned char* handles, int rank, int world);
+
 void mr_als_destroy(mr_als* ctx);
 
 /* Factor tables in the reference layout: U[num_users*(k+1)] (row = k factors,

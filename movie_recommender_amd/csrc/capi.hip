@@ -218,6 +218,16 @@ int mr_als_set_rccl(mr_als* ctx, const unsigned char id[128], int rank, int worl
   });
 }
 
+int mr_als_peer_handle(mr_als* ctx, unsigned char out[64]) {
+  MR_CHECK(ctx && out, "null argument");
+  return guarded([&]() { return ctx->eng.peer_handle(out); });
+}
+
+int mr_als_set_peer(mr_als* ctx, const unsigned char* handles, int rank, int world) {
+  MR_CHECK(ctx && handles, "null argument");
+  return guarded([&]() { return ctx->eng.set_peer(handles, rank, world); });
+}
+
 void mr_als_destroy(mr_als* ctx) { delete ctx; }
 
 int mr_als_set_factors(mr_als* ctx, const double* U, const double* V) {

@@ -97,6 +97,11 @@ struct Engine {
   std::vector<long long> row_begin_u, row_begin_i;
   AgStage ag_u, ag_i;
   std::vector<float> h_ag;   // host staging of the padded exchange (callback transport)
+  // peer all-reduce of the CG scalars (include/mr_als.h mr_als_set_peer)
+  double* peer_buf = nullptr;            // this rank's exchange buffer (uncached)
+  PeerComm* d_peer = nullptr;
+  std::vector<void*> peer_opened;        // peers' buffers mapped by IPC
+  bool peer_on = false;
 
   ~Engine();
   int init(int dev, int k, int64_t U, int64_t I, int64_t n_u, const int* uv_uid,
@@ -113,6 +118,8 @@ struct Engine {
   // single-rank) or host callbacks with more than one rank.
   bool sharded() const { return rccl != nullptr || (has_comm && comm.world > 1); }
   int set_rccl(const unsigned char* id, int rank, int world);
+  int peer_handle(unsigned char* out64);
+  int set_peer(const unsigned char* handles, int rank, int world);
   // padded all-gather staging (both transports): every shard padded to the
   // largest one; needs row_begin_u / row_begin_i
   int alloc_ag(int world);

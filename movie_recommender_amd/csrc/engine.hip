@@ -76,6 +76,9 @@ Engine::~Engine() {
       dfree(A->recv_b, stream); dfree(A->rb, stream);
     }
     dfree(d_state, stream); dfree(partials, stream); dfree(d_flag, stream);
+    dfree(d_peer, stream);
+    for (void* q : peer_opened) (void)hipIpcCloseMemHandle(q);
+    if (peer_buf) (void)hipFree(peer_buf);
     (void)hipStreamSynchronize(stream);
     if (h_state) (void)hipHostFree(h_state);
     if (h_init) (void)hipHostFree(h_init);
@@ -454,6 +457,58 @@ int Engine::set_rccl(const unsigned char* id, int rank, int world) {
   return alloc_ag(world);
 }
 
+// Peer all-reduce of the CG scalars: this rank's exchange buffer (kPeerSlots x
+// kMaxPeers records of 4 doubles, uncached device memory so that peers'
+// stores over xGMI are seen by this GPU's loads) and its IPC handle.
+int Engine::peer_handle(unsigned char* out64) {
+  static_assert(sizeof(hipIpcMemHandle_t) == 64, "hipIpcMemHandle_t size");
+  MR_HIP(hipSetDevice(device));
+  if (!peer_buf) {
+    const size_t bytes = (size_t)kPeerSlots * kMaxPeers * 4 * sizeof(double);
+    MR_HIP(hipExtMallocWithFlags((void**)&peer_buf, bytes, hipDeviceMallocUncached));
+    MR_HIP(hipMemsetAsync(peer_buf, 0, bytes, stream));
+    MR_HIP(hipStreamSynchronize(stream));
+  }
+  hipIpcMemHandle_t h;
+  MR_HIP(hipIpcGetMemHandle(&h, peer_buf));
+  memcpy(out64, &h, 64);
+  return 0;
+}
+
+// Map every peer's exchange buffer and switch the CG scalars to the peer
+// all-reduce: the finalizing thread of each reduction exchanges its sum with
+// the peers itself, so a sharded CG iteration issues the unsharded launch
+// sequence (matvec, update) with no collective launch in between.  All
+// ranks must call this (after exchanging the handles of peer_handle) before
+// their next solve; the factor all-gather keeps its transport.
+int Engine::set_peer(const unsigned char* handles, int rank, int world) {
+  MR_CHECK(world >= 1 && world <= kMaxPeers && rank >= 0 && rank < world, "bad rank/world");
+  MR_CHECK(peer_buf, "mr_als_peer_handle must be called first");
+  MR_HIP(hipSetDevice(device));
+  PeerComm pc{};
+  pc.world = world;
+  pc.rank = rank;
+  for (int q = 0; q < world; ++q) {
+    if (q == rank) {
+      pc.buf[q] = peer_buf;
+      continue;
+    }
+    hipIpcMemHandle_t h;
+    memcpy(&h, handles + (size_t)q * 64, 64);
+    void* ptr = nullptr;
+    MR_HIP(hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess));
+    peer_opened.push_back(ptr);
+    pc.buf[q] = (double*)ptr;
+  }
+  if (!d_peer && dalloc(&d_peer, 1, stream)) return -1;
+  MR_H2D(d_peer, &pc, sizeof(PeerComm), stream);
+  PeerComm* dp = d_peer;
+  MR_H2D((char*)d_state + offsetof(CgState, peer), &dp, sizeof(dp), stream);
+  MR_HIP(hipStreamSynchronize(stream));
+  peer_on = true;
+  return 0;
+}
+
 // All-gather staging, the same for both transports: every rank's shard padded
 // to the largest one (maxrows rows of ldk floats, + the user bias column).
 // Row boundaries are checked here, on the host, against everything the pack /
@@ -694,17 +749,20 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr, bool start
   const int64_t n = S.E * ldk;
   const int64_t nb = user ? S.E : 0;
   const size_t pend0 = pending.size();
+  // peer all-reduce: the scalars are exchanged inside the finalizing thread,
+  // so the CG runs the unsharded launch protocol (no collective launches)
+  const bool shard = sharded() && !peer_on;
   memset(h_init, 0, sizeof(CgState));
   h_init->min_dec = min_dec;
   h_init->max_it = max_it;
-  h_init->sharded = sharded() ? 1 : 0;
+  h_init->sharded = shard ? 1 : 0;
+  h_init->peer = peer_on ? d_peer : nullptr;
   // The control steps run in the last-arriving block of the matvec (alpha)
   // and of the update (INIT / BETA rules + publish): two kernels per
   // iteration.  Sharded runs: those blocks only sum the local partials into
   // the state slot, RCCL all-reduces it, the update derives alpha from the
   // reduced slot itself, and a one-block finalize applies the INIT / BETA
   // rules -- three kernels and two all-reduces per iteration.
-  const bool shard = sharded();
   CgState* fst = d_state;
   hipEvent_t a = nullptr;
   const int seq_init = ++mirror_seq;
@@ -839,6 +897,7 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr, bool start
     MR_CHECK(known <= max_it, "CG did not terminate");
   }
   for (size_t i = pend0; i < pending.size(); ++i) pending[i].n_real = ms.n_matvec;
+  MR_CHECK(ms.ret >= 0, "peer all-reduce of the CG scalars timed out (a rank did not arrive)");
   if (final_rr) *final_rr = ms.final_rr;
   return ms.ret;
 }

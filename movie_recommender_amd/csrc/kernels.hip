@@ -1543,8 +1543,61 @@ __device__ __forceinline__ void apply_beta(CgScalars& v, double rr2) {
   }
 }
 
+// Peer all-reduce of `count` (<= 2) doubles by ONE thread (the finalizing
+// thread of a kernel whose blocks have all finished): write this rank's
+// values into its record of every rank's exchange buffer, tag it with the
+// reduction's sequence number (release, system scope), wait for the tags of
+// all ranks' records in the own buffer (acquire), sum in rank order.  Every
+// rank issues the same reductions in the same order (the exact-state launch
+// protocol), so sequence numbers agree; a slot is reused only after every
+// rank has passed kPeerSlots - 1 later reductions, each of which needed this
+// rank's data, so no record is overwritten before it is read.  A peer that
+// does not arrive within ~30 s sets `error` and the caller ends the solve
+// with ret = -1 (the host reports it) instead of spinning forever.
+// Returns false on timeout.
+__device__ bool peer_sum(PeerComm* pc, double* vals, int count) {
+  const uint32_t s = pc->seq + 1;
+  pc->seq = s;
+  const int world = pc->world, rank = pc->rank;
+  const int64_t slot = s % kPeerSlots;
+  for (int q = 0; q < world; ++q) {
+    double* rec = pc->buf[q] + (slot * world + rank) * 4;
+    for (int c = 0; c < count; ++c)
+      __hip_atomic_store(rec + c, vals[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(rec + 3), (uint64_t)s, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  double acc[2] = {0.0, 0.0};
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
+  for (int q = 0; q < world; ++q) {
+    const double* rec = pc->buf[rank] + (slot * world + q) * 4;
+    while (__hip_atomic_load(reinterpret_cast<const uint64_t*>(rec + 3), __ATOMIC_ACQUIRE,
+                             __HIP_MEMORY_SCOPE_SYSTEM) != (uint64_t)s) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 3000000000ull) {
+        pc->error = 1;
+        return false;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    for (int c = 0; c < count; ++c)
+      acc[c] += __hip_atomic_load(rec + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  for (int c = 0; c < count; ++c) vals[c] = acc[c];
+  return true;
+}
+
+// A failed peer exchange ends the solve (every later kernel is a no-op) with
+// ret = -1, published so the host's wait returns.
+__device__ void peer_fail(CgState* st, CgMirror* mirror, int seq);
+
 // INIT / ALPHA / BETA rules on the reduced sum s (one thread).
 __device__ void cg_finalize(CgState* st, int phase, double s, CgMirror* mirror, int seq) {
+  if (PeerComm* pc = ald(&st->peer)) {
+    if (!peer_sum(pc, &s, 1)) {
+      peer_fail(st, mirror, seq);
+      return;
+    }
+  }
   CgScalars v = load_state(st);
   if (phase == CG_INIT) {
     v.rr = s;
@@ -1565,6 +1618,14 @@ __device__ void cg_finalize(CgState* st, int phase, double s, CgMirror* mirror, 
     store_state(st, v);
     publish(v, mirror, seq);
   }
+}
+
+__device__ void peer_fail(CgState* st, CgMirror* mirror, int seq) {
+  CgScalars v = load_state(st);
+  v.done = 1;
+  v.ret = -1;
+  store_state(st, v);
+  publish(v, mirror, seq);
 }
 
 // Sharded runs: the BETA step of iteration t (its r.r all-reduced into
@@ -2087,8 +2148,16 @@ __global__ __launch_bounds__(CTL_THREADS) void cg_control_kernel(
       __syncthreads();
       const double tb = block_sum_f64<CTL_THREADS>(b, sh);
       if (threadIdx.x == 0) {
-        ast(&st->comm[0], ta);
-        ast(&st->comm[1], tb);
+        double t2[2] = {ta, tb};
+        PeerComm* pc = ald(&st->peer);
+        if (pc && (ctl & CTL_FINALIZE) && !peer_sum(pc, t2, 2)) {
+          ast(&st->comm[0], 0.0);
+          ast(&st->comm[1], 0.0);
+          peer_fail(st, mirror, seq);
+          return;
+        }
+        ast(&st->comm[0], t2[0]);
+        ast(&st->comm[1], t2[1]);
       }
     } else {
       double acc = 0.0;

@@ -172,6 +172,22 @@ struct CgStart {
   double* parts;
 };
 
+// Peer all-reduce of the CG scalars over IPC-mapped device memory (sharded
+// runs; Engine::set_peer).  Every rank owns an exchange buffer of
+// kPeerSlots x world records {v0, v1, -, tag} in uncached device memory and
+// maps every peer's.  Reduction s writes this rank's values into record
+// (s % kPeerSlots, rank) of EVERY rank's buffer, then the tag s (release,
+// system scope); each rank then waits for the tag of every record of its own
+// buffer and sums the values in rank order -- so all ranks get the same bits.
+constexpr int kPeerSlots = 16;
+constexpr int kMaxPeers = 64;
+struct PeerComm {
+  int32_t world, rank;
+  uint32_t seq;            // reductions done (advanced by the reducing thread)
+  int32_t error;           // 1: a peer did not arrive within the timeout
+  double* buf[kMaxPeers];  // rank q's exchange buffer, mapped into this process
+};
+
 // CG scalar state, device resident (matrix.cpp:456-529 scalars).
 struct CgState {
   double rr;        // r.r of the current iterate
@@ -188,6 +204,8 @@ struct CgState {
   int32_t n_matvec; // matvec launches that did work (for kernel timing)
   uint32_t arrive;  // blocks finished (fused control: the last one finalizes)
   int32_t sharded;  // 1: the last block only sums into comm[0] for the all-reduce
+  PeerComm* peer;   // non-null: the finalizing thread all-reduces its sum with
+                    // the peers itself (no collective launches; rules as unsharded)
 };
 
 // Host-visible copies of the CG state: a ring of kMirrorSlots records in

@@ -152,13 +152,43 @@ def attach_rccl(ctx, rank, world, user_begin, item_begin):
     ctx._rccl = (ub, ib)
 
 
+def attach_peer_scalars(ctx, rank, world):
+    """Switch ``ctx``'s CG scalars to the peer all-reduce (include/mr_als.h
+    ``mr_als_set_peer``): every rank exports its exchange buffer's IPC handle,
+    ``torch.distributed`` gathers the handles in rank order, every rank maps
+    its peers'.  Collective: all ranks call it.  Returns True on success;
+    on any rank's failure every rank keeps its collective scalars (the
+    outcome is agreed by an all-reduce first)."""
+    import torch
+    import torch.distributed as dist
+    L = _lib.lib()
+    buf = ctypes.create_string_buffer(64)
+    ok = L.mr_als_peer_handle(ctx._h, buf) == 0
+    handles = [None] * world
+    dist.all_gather_object(handles, bytes(buf.raw) if ok else None)
+    if any(h is None for h in handles):
+        return False
+    joined = ctypes.create_string_buffer(b"".join(handles), 64 * world)
+    ok = L.mr_als_set_peer(ctx._h, joined, int(rank), int(world)) == 0
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    if dist.get_backend() == "nccl":
+        flag = flag.cuda()
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) != 1:
+        raise RuntimeError("peer scalar all-reduce could not be set up on every rank: "
+                           + _lib.last_error())
+    ctx._peer = joined
+    return True
+
+
 def sharded_context(user_ids, item_ids, ratings, k, num_users, num_items, device,
-                    comm="rccl", bounds=None, **kw):
+                    comm="rccl", bounds=None, scalars="collective", **kw):
     """Build this rank's ``AlsContext`` over an initialised torch.distributed
     group and attach its collectives: ``comm="rccl"`` (native, device-side),
     or a ``TorchComm`` (host-staged callbacks carrying the same padded
     exchange buffers; works with gloo).  ``bounds=(ub, ib)`` imposes the
-    shard boundaries (default: cost-balanced)."""
+    shard boundaries (default: cost-balanced).  ``scalars="peer"``: the CG
+    scalars go through the peer all-reduce (``attach_peer_scalars``)."""
     import torch.distributed as dist
     from .engine import AlsContext
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -171,4 +201,6 @@ def sharded_context(user_ids, item_ids, ratings, k, num_users, num_items, device
     else:
         ctx.set_comm(comm.struct, ub, ib)
         ctx._comm_owner = comm
+    if scalars == "peer":
+        attach_peer_scalars(ctx, rank, world)
     return ctx

@@ -12,6 +12,8 @@ Modes
                (the same padded device exchange buffers as RCCL: pack_rows
                -> all-gather -> unstage_rows); --skew imposes uneven shards.
   engine_rccl  the HIP engine with its native RCCL communicator.
+  engine_peer  engine_gloo with the CG scalars through the peer all-reduce
+               (IPC-mapped exchange buffers, include/mr_als.h mr_als_set_peer).
 """
 import argparse
 import os
@@ -99,7 +101,7 @@ def engine_sharded(d, max_iteration, rank, world, mode, skew=False):
     nU, nI = int(d["num_users"]), int(d["num_items"])
     bounds = (skewed_bounds(nU, world), skewed_bounds(nI, world)) if skew else None
     ctx = sharded_context(d["user_ids"], d["item_ids"], d["ratings"], k, nU, nI, dev, comm,
-                          bounds=bounds)
+                          bounds=bounds, scalars="peer" if mode == "engine_peer" else "collective")
     ctx.set_factors(d["U0"], d["V0"])
     ret = ctx.run(0.01, max_iteration)
     U, V = ctx.get_factors()

@@ -263,3 +263,27 @@ def test_pack_rows_matches_slice(gpu):
                                        send_b.ctypes.data_as(_lib.FP)), "mr_test_pack_rows")
         assert np.array_equal(send[:n * ldk], fac[r0 * ldk:(r0 + n) * ldk])
         assert np.array_equal(send_b[:n], bias[r0:r0 + n])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fixture,max_it,nproc,skew", [
+    ("als_dense_300x260_k64.npz", 200, 2, False),
+    ("als_mlshape_k64_it4.npz", 4, 2, False),
+    ("als_dense_200x150_k32.npz", 200, 3, True),
+    ("als_dense_400x300_k128.npz", 200, 3, False)])
+def test_engine_peer_scalars_match_collective(gpu, tmp_path, fixture, max_it, nproc, skew):
+    """The CG scalars through the peer all-reduce (exchange buffers mapped by
+    hipIpcOpenMemHandle between the rank processes, here all on one GPU;
+    each rank sums the records in rank order) against the same sharded run
+    with the scalars through the gloo callbacks: at world 2 bit for bit (a
+    sum of two terms is the same in either order), at world 3 within the
+    reference tolerance; both against the compiled reference's golden."""
+    d = load_golden(fixture)
+    Up, Vp, retp = run_workers("engine_peer", fixture, nproc, tmp_path, max_it, skew=skew)
+    Ug, Vg, retg = run_workers("engine_gloo", fixture, nproc, tmp_path, max_it, skew=skew)
+    assert retp == retg == int(d["ret"])
+    if nproc == 2:
+        assert np.array_equal(Up, Ug) and np.array_equal(Vp, Vg)
+    else:
+        assert rel_err(Up, Ug) < 1e-5 and rel_err(Vp, Vg) < 1e-5
+    assert rel_err(Up, d["U"]) < 1e-5 and rel_err(Vp, d["V"]) < 1e-5
