@@ -241,6 +241,9 @@ def main():
                     help="reference threads (default: this process's CPU share)")
     ap.add_argument("--force-shard", action="store_true",
                     help="use the sharded RCCL path even with one rank (testing)")
+    ap.add_argument("--scalars", default="peer", choices=["peer", "collective"],
+                    help="sharded runs: CG scalars through the peer all-reduce (IPC-mapped "
+                         "buffers; falls back to RCCL if its self-test fails) or RCCL")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r02.json"),
                     help="per-kernel HBM bytes from a rocprofv3 --pmc run (optional)")
     args = ap.parse_args()
@@ -290,6 +293,9 @@ def main():
                              item_range=(i0, i1), item_view=iv)
             del uv, iv
             attach_rccl(ctx, rank, world, ub, ib)
+            if args.scalars == "peer":
+                from movie_recommender_amd.distributed import attach_peer_scalars
+                ctx.peer_scalars = attach_peer_scalars(ctx, rank, world)
         else:
             u, i, r = gen.all_ratings()
             ctx = AlsContext(u, i, r, k, n_users, n_items, device=local_rank,
@@ -302,7 +308,8 @@ def main():
         V0 = rng.uniform(-1, 1, n_items * k)
         if dist is not None:
             ctx = sharded_context(rs.user_ids, rs.item_ids, rs.ratings, k, n_users, n_items,
-                                  local_rank, "rccl", solver=args.solver, ridge=args.ridge)
+                                  local_rank, "rccl", solver=args.solver, ridge=args.ridge,
+                                  scalars=args.scalars)
         else:
             ctx = AlsContext(rs.user_ids, rs.item_ids, rs.ratings, k, n_users, n_items,
                              device=local_rank, solver=args.solver, ridge=args.ridge)
@@ -442,7 +449,9 @@ def main():
                    "k": k, "n_ratings": int(n_total), "users": int(n_users),
                    "items": int(n_items), "solver": args.solver,
                    "parallelism": (f"shard{world}" if world > 1 or args.force_shard
-                                   else "single")},
+                                   else "single"),
+                   "cg_scalars": ("peer all-reduce (IPC)" if getattr(ctx, "peer_scalars", False)
+                                  else "rccl all-reduce" if dist is not None else "local")},
         "roofline": {"kernel": cls, "bound": bound, "achieved": round(achieved, 2),
                      "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
                      "traffic": traffic,

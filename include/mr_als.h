@@ -109,7 +109,8 @@ int mr_als_set_comm(mr_als* ctx, const mr_comm* comm,
  * an id with mr_rccl_unique_id and every rank passes the same 128 bytes.
  * All ranks must call mr_als_set_rccl concurrently (it builds the RCCL
  * communicator).  The CG scalars are then all-reduced on the device stream
- * and factor shards exchanged by grouped in-place broadcasts. */
+ * and the factor shards exchanged by one all-gather of equal, padded shards
+ * per half-step. */
 int mr_rccl_unique_id(unsigned char out[128]);
 int mr_als_set_rccl(mr_als* ctx, const unsigned char id[128], int rank, int world,
                     const long long* user_begin, const long long* item_begin);
@@ -123,9 +124,12 @@ int mr_als_set_rccl(mr_als* ctx, const unsigned char id[128], int rank, int worl
  * mr_als_peer_handle (64 bytes), exchange them (rank order), then
  * mr_als_set_peer with the world x 64 bytes.  Reference scalars:
  * matrix.cpp:485, 497, 507.  A peer that does not arrive within ~30 s fails
- * the solve (< 0) instead of hanging. */
+ * the solve (< 0) instead of hanging.  mr_als_set_peer with world = 0
+ * switches back to the collective scalars.  mr_als_peer_selftest (all ranks
+ * together) runs one reduction of {rank + 1, 1} and checks the sums. */
 int mr_als_peer_handle(mr_als* ctx, unsigned char out[64]);
 int mr_als_set_peer(mr_als* ctx, const unsigned char* handles, int rank, int world);
+int mr_als_peer_selftest(mr_als* ctx);
 
 void mr_als_destroy(mr_als* ctx);
 

@@ -228,6 +228,11 @@ int mr_als_set_peer(mr_als* ctx, const unsigned char* handles, int rank, int wor
   return guarded([&]() { return ctx->eng.set_peer(handles, rank, world); });
 }
 
+int mr_als_peer_selftest(mr_als* ctx) {
+  MR_CHECK(ctx, "null context");
+  return guarded([&]() { return ctx->eng.peer_selftest(); });
+}
+
 void mr_als_destroy(mr_als* ctx) { delete ctx; }
 
 int mr_als_set_factors(mr_als* ctx, const double* U, const double* V) {

@@ -6,7 +6,8 @@
 // Per context: A uploaded once (CSR, int64 offsets on the device), its
 // explicit transpose built on the device (sparse_matrix_transpose,
 // matrix.cpp:617-692, as a stable radix sort), and the CSR-stream row blocks
-// of both.  Per solve: b2 = A^T b, r0 = A^T A x - b2, p0 = -r0, then three
+// of both; A's rows are held ordered by first column (a row permutation,
+// b permuted alike per solve).  Per solve: b2 = A^T b, r0 = A^T A x - b2, p0 = -r0, then three
 // kernels per CG iteration (kernels.hip: csr_spmv_kernel x 2, cgls_update);
 // the scalars and stop rules live in the device CgState and every BETA step
 // publishes the state into a host-mapped seqlock ring (as the ALS engine), so
@@ -59,9 +60,9 @@ struct CgLs {
   std::vector<void*> owned;
   int64_t *rp = nullptr, *tp = nullptr, *blk_a = nullptr, *blk_t = nullptr;
   int64_t n_blk_a = 0, n_blk_t = 0;
-  int32_t *ci = nullptr, *ti = nullptr;
+  int32_t *ci = nullptr, *ti = nullptr, *perm = nullptr;
   double *v = nullptr, *tv = nullptr;
-  double *b = nullptr, *b2 = nullptr, *x = nullptr, *r = nullptr, *p = nullptr, *q = nullptr,
+  double *b_in = nullptr, *b = nullptr, *b2 = nullptr, *x = nullptr, *r = nullptr, *p = nullptr, *q = nullptr,
          *t = nullptr, *partials = nullptr;
   CgState* st = nullptr;
   CgState* h_init = nullptr;
@@ -134,9 +135,12 @@ struct CgLs {
                          hipHostMallocMapped | hipHostMallocCoherent));
     memset(h_mirror, 0, kMirrorSlots * sizeof(CgMirror));
     MR_HIP(hipHostGetDevicePointer((void**)&d_mirror, h_mirror, 0));
-    int32_t *rp32 = nullptr, *rowof = nullptr;
+    int32_t *rp32 = nullptr, *rowof = nullptr, *ci0 = nullptr;
+    int64_t* rp0 = nullptr;
+    double* v0 = nullptr;
     if (dmalloc(&rp, rows + 1, owned) || dmalloc(&ci, nnz, owned) || dmalloc(&v, nnz, owned) ||
-        dmalloc(&tp, cols + 1, owned) || dmalloc(&ti, nnz, owned) || dmalloc(&tv, nnz, owned) ||
+        dmalloc(&perm, rows, owned) || dmalloc(&tp, cols + 1, owned) ||
+        dmalloc(&ti, nnz, owned) || dmalloc(&tv, nnz, owned) || dmalloc(&b_in, rows, owned) ||
         dmalloc(&b, rows, owned) || dmalloc(&t, rows, owned) || dmalloc(&b2, cols, owned) ||
         dmalloc(&x, cols, owned) || dmalloc(&r, cols, owned) || dmalloc(&p, cols, owned) ||
         dmalloc(&q, cols, owned) || dmalloc(&partials, kMaxParts, owned) ||
@@ -151,19 +155,32 @@ struct CgLs {
         for (void* q_ : v) (void)hipFree(q_);
       }
     } tmp_free{tmp, s};
-    if (dmalloc(&rp32, rows + 1, tmp) || dmalloc(&rowof, nnz, tmp)) return -1;
+    if (dmalloc(&rp32, rows + 1, tmp) || dmalloc(&rp0, rows + 1, tmp) ||
+        dmalloc(&ci0, nnz, tmp) || dmalloc(&v0, nnz, tmp))
+      return -1;
     MR_H2D(rp32, hrp, (rows + 1) * 4, s);
     if (nnz) {
-      MR_H2D(ci, hci, nnz * 4, s);
-      MR_H2D(v, hv, nnz * 8, s);
+      MR_H2D(ci0, hci, nnz * 4, s);
+      MR_H2D(v0, hv, nnz * 8, s);
     }
-    if (launch_i32_to_i64(s, rows + 1, rp32, rp)) return -1;
+    if (launch_i32_to_i64(s, rows + 1, rp32, rp0)) return -1;
+    // rows ordered by first column (a row permutation: same solution, same
+    // row sums), so A^T's rows read t in runs and A's rows gather r, p from
+    // neighbouring columns (csr_build.hip sort_rows_by_first_col)
+    if (sort_rows_by_first_col(s, rows, cols, rp0, ci0, v0, perm, rp, ci, v)) return -1;
+    for (void* q_ : {(void*)rp32, (void*)rp0, (void*)ci0, (void*)v0}) {
+      (void)hipStreamSynchronize(s);
+      (void)hipFree(q_);
+    }
+    tmp.clear();
+    if (dmalloc(&rowof, nnz, tmp)) return -1;
     // explicit transpose (sparse_matrix_transpose, matrix.cpp:617-692): a
     // stable sort of the non-zeros by column keeps each column's rows in order
     if (launch_rows_of(s, rows, rp, rowof)) return -1;
     if (build_csr<double, double>(s, nnz, cols, ci, 0, rowof, v, tp, ti, tv)) return -1;
-    // row blocks of A (host offsets) and of A^T (offsets read back once)
-    std::vector<int64_t> offa(hrp, hrp + rows + 1), offt(cols + 1);
+    // row blocks of A and of A^T (offsets read back once)
+    std::vector<int64_t> offa(rows + 1), offt(cols + 1);
+    MR_D2H(offa.data(), rp, (rows + 1) * 8, s);
     MR_D2H(offt.data(), tp, (cols + 1) * 8, s);
     const std::vector<int64_t> ba = row_blocks(offa), bt = row_blocks(offt);
     n_blk_a = (int64_t)ba.size() - 1;
@@ -205,7 +222,10 @@ struct CgLs {
 
   int solve(const double* hb, double* hx, double min_dec, int max_it, double* final_rr) {
     MR_HIP(hipSetDevice(device));
-    if (rows) MR_H2D(b, hb, rows * 8, s);
+    if (rows) {
+      MR_H2D(b_in, hb, rows * 8, s);
+      if (launch_gather_f64(s, rows, perm, b_in, b)) return -1;   // b in the rows' order
+    }
     if (cols) MR_H2D(x, hx, cols * 8, s);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (timing) {

@@ -7,6 +7,7 @@
 // (rocPRIM onesweep), then the opposite ids and values are gathered and the
 // row offsets are derived from the sorted keys.  Stability keeps every
 // entity's ratings in input order, so runs are reproducible.
+#include <algorithm>
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 
@@ -102,6 +103,96 @@ int build_csr(hipStream_t s, int64_t n, int64_t E, const int32_t* d_key,
   if (v0) (void)hipFree(v0);
   if (v1) (void)hipFree(v1);
   if (rc != 0) set_error("build_csr: device sort failed (out of memory?)");
+  return rc;
+}
+
+// ---------------------------------------------------------------------------
+// Row locality for the general least squares (cgls.hip): rows of a CSR
+// matrix stably sorted by their first column id (empty rows last), and the
+// matrix rebuilt in that row order.  A^T's rows (the columns of A) then list
+// runs of consecutive permuted rows, so the A^T SpMV reads t in order instead
+// of gathering it at random; a row permutation leaves the least-squares
+// solution and every row sum unchanged (only A^T's summation order moves).
+// ---------------------------------------------------------------------------
+__global__ void first_col_kernel(int64_t rows, int64_t cols, const int64_t* __restrict__ rp,
+                                 const int32_t* __restrict__ ci, uint32_t* __restrict__ key,
+                                 int32_t* __restrict__ id) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    key[r] = rp[r + 1] > rp[r] ? (uint32_t)ci[rp[r]] : (uint32_t)cols;
+    id[r] = (int32_t)r;
+  }
+}
+
+__global__ void perm_len_kernel(int64_t rows, const int32_t* __restrict__ perm,
+                                const int64_t* __restrict__ rp, int64_t* __restrict__ len) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = perm[i];
+    len[i] = rp[r + 1] - rp[r];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) len[rows] = 0;
+}
+
+// 8 lanes per row copy its non-zeros to the row's new position
+__global__ void perm_copy_kernel(int64_t rows, const int32_t* __restrict__ perm,
+                                 const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                                 const double* __restrict__ v, const int64_t* __restrict__ rp2,
+                                 int32_t* __restrict__ ci2, double* __restrict__ v2) {
+  const int sub = threadIdx.x & 7;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3; i < rows;
+       i += ((int64_t)gridDim.x * blockDim.x) >> 3) {
+    const int64_t r = perm[i], a = rp[r], n = rp[r + 1] - a, d = rp2[i];
+    for (int64_t j = sub; j < n; j += 8) {
+      ci2[d + j] = ci[a + j];
+      v2[d + j] = v[a + j];
+    }
+  }
+}
+
+int sort_rows_by_first_col(hipStream_t s, int64_t rows, int64_t cols, const int64_t* rp,
+                           const int32_t* ci, const double* v, int32_t* perm, int64_t* rp2,
+                           int32_t* ci2, double* v2) {
+  MR_CHECK(rows < ((int64_t)1 << 31) && cols < ((int64_t)1 << 31), "matrix too large");
+  if (rows == 0) {
+    MR_HIP(hipMemsetAsync(rp2, 0, sizeof(int64_t), s));
+    return 0;
+  }
+  int bits = 1;
+  while (((int64_t)1 << bits) <= cols) ++bits;
+  uint32_t *k0 = nullptr, *k1 = nullptr;
+  int32_t* v0 = nullptr;
+  int64_t* len = nullptr;
+  void* tmp = nullptr;
+  size_t tb = 0, tb2 = 0;
+  int rc = -1;
+  do {
+    if (hipMalloc((void**)&k0, rows * 4) != hipSuccess) break;
+    if (hipMalloc((void**)&k1, rows * 4) != hipSuccess) break;
+    if (hipMalloc((void**)&v0, rows * 4) != hipSuccess) break;
+    if (hipMalloc((void**)&len, (rows + 1) * 8) != hipSuccess) break;
+    first_col_kernel<<<grid_of(rows), 256, 0, s>>>(rows, cols, rp, ci, k0, v0);
+    if (rocprim::radix_sort_pairs(nullptr, tb, k0, k1, v0, perm, (size_t)rows, 0, bits, s) !=
+        hipSuccess) break;
+    if (rocprim::exclusive_scan(nullptr, tb2, len, rp2, (int64_t)0, (size_t)rows + 1,
+                                rocprim::plus<int64_t>(), s) != hipSuccess) break;
+    if (hipMalloc(&tmp, std::max(tb, tb2)) != hipSuccess) break;
+    if (rocprim::radix_sort_pairs(tmp, tb, k0, k1, v0, perm, (size_t)rows, 0, bits, s) !=
+        hipSuccess) break;
+    perm_len_kernel<<<grid_of(rows), 256, 0, s>>>(rows, perm, rp, len);
+    if (rocprim::exclusive_scan(tmp, tb2, len, rp2, (int64_t)0, (size_t)rows + 1,
+                                rocprim::plus<int64_t>(), s) != hipSuccess) break;
+    perm_copy_kernel<<<grid_of(rows * 8), 256, 0, s>>>(rows, perm, rp, ci, v, rp2, ci2, v2);
+    if (hipGetLastError() != hipSuccess) break;
+    rc = 0;
+  } while (0);
+  (void)hipStreamSynchronize(s);
+  if (tmp) (void)hipFree(tmp);
+  if (k0) (void)hipFree(k0);
+  if (k1) (void)hipFree(k1);
+  if (v0) (void)hipFree(v0);
+  if (len) (void)hipFree(len);
+  if (rc != 0) set_error("sort_rows_by_first_col: device sort failed (out of memory?)");
   return rc;
 }
 

@@ -482,6 +482,15 @@ int Engine::peer_handle(unsigned char* out64) {
 // ranks must call this (after exchanging the handles of peer_handle) before
 // their next solve; the factor all-gather keeps its transport.
 int Engine::set_peer(const unsigned char* handles, int rank, int world) {
+  if (world == 0) {   // back to the collective scalars (e.g. a failed self-test)
+    MR_HIP(hipSetDevice(device));
+    PeerComm* none = nullptr;
+    MR_H2D((char*)d_state + offsetof(CgState, peer), &none, sizeof(none), stream);
+    MR_HIP(hipStreamSynchronize(stream));
+    peer_on = false;
+    return 0;
+  }
+  MR_CHECK(handles, "null handles");
   MR_CHECK(world >= 1 && world <= kMaxPeers && rank >= 0 && rank < world, "bad rank/world");
   MR_CHECK(peer_buf, "mr_als_peer_handle must be called first");
   MR_HIP(hipSetDevice(device));
@@ -506,6 +515,26 @@ int Engine::set_peer(const unsigned char* handles, int rank, int world) {
   MR_H2D((char*)d_state + offsetof(CgState, peer), &dp, sizeof(dp), stream);
   MR_HIP(hipStreamSynchronize(stream));
   peer_on = true;
+  return 0;
+}
+
+// One reduction of {rank + 1, 1} through the mapped buffers (collective: all
+// ranks call it): 0 if every rank's record arrived and the sums are right.
+int Engine::peer_selftest() {
+  MR_CHECK(peer_on && d_peer, "peer all-reduce not set up");
+  MR_HIP(hipSetDevice(device));
+  double* d_out = nullptr;
+  if (dalloc(&d_out, 3, stream)) return -1;
+  double out[3] = {0, 0, 0};
+  int rc = launch_peer_selftest(stream, d_peer, d_out);
+  if (!rc) rc = t_stager.d2h(stream, out, d_out, sizeof(out));
+  dfree(d_out, stream);
+  if (rc) return -1;
+  PeerComm pc{};
+  MR_D2H(&pc, d_peer, sizeof(PeerComm), stream);
+  const double w = pc.world;
+  MR_CHECK(out[2] == 1.0, "peer all-reduce self-test: a rank did not arrive");
+  MR_CHECK(out[0] == w * (w + 1) / 2 && out[1] == w, "peer all-reduce self-test: wrong sum");
   return 0;
 }
 

@@ -1586,6 +1586,23 @@ __device__ bool peer_sum(PeerComm* pc, double* vals, int count) {
   return true;
 }
 
+// Self-test of a freshly mapped peer exchange: one reduction of
+// {rank + 1, 1}; out = {sum, count, ok}.  Run by every rank at attach time.
+__global__ void peer_selftest_kernel(PeerComm* pc, double* out) {
+  if (threadIdx.x != 0) return;
+  double v[2] = {(double)(pc->rank + 1), 1.0};
+  const bool ok = peer_sum(pc, v, 2);
+  out[0] = v[0];
+  out[1] = v[1];
+  out[2] = ok ? 1.0 : 0.0;
+}
+
+int launch_peer_selftest(hipStream_t s, PeerComm* pc, double* out) {
+  peer_selftest_kernel<<<1, 64, 0, s>>>(pc, out);
+  MR_HIP(hipGetLastError());
+  return 0;
+}
+
 // A failed peer exchange ends the solve (every later kernel is a no-op) with
 // ret = -1, published so the host's wait returns.
 __device__ void peer_fail(CgState* st, CgMirror* mirror, int seq);
@@ -2672,6 +2689,20 @@ int launch_gather_i32(hipStream_t s, int64_t n, const int64_t* pos, const int32_
                       int32_t* dst) {
   if (n <= 0) return 0;
   gather_i32_kernel<<<grid_for(n), 256, 0, s>>>(n, pos, src, dst);
+  MR_HIP(hipGetLastError());
+  return 0;
+}
+
+__global__ void gather_f64_kernel(int64_t n, const int32_t* __restrict__ pos,
+                                  const double* __restrict__ src, double* __restrict__ dst) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n;
+       t += (int64_t)gridDim.x * blockDim.x)
+    dst[t] = src[pos[t]];
+}
+int launch_gather_f64(hipStream_t s, int64_t n, const int32_t* pos, const double* src,
+                      double* dst) {
+  if (n <= 0) return 0;
+  gather_f64_kernel<<<grid_for(n), 256, 0, s>>>(n, pos, src, dst);
   MR_HIP(hipGetLastError());
   return 0;
 }

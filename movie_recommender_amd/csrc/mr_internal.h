@@ -188,6 +188,9 @@ struct PeerComm {
   double* buf[kMaxPeers];  // rank q's exchange buffer, mapped into this process
 };
 
+// One peer reduction of {rank + 1, 1} into out[0..2] = {sum, count, ok}.
+int launch_peer_selftest(hipStream_t s, PeerComm* pc, double* out);
+
 // CG scalar state, device resident (matrix.cpp:456-529 scalars).
 struct CgState {
   double rr;        // r.r of the current iterate
@@ -322,6 +325,9 @@ int launch_i32_to_i64(hipStream_t s, int64_t n, const int32_t* in, int64_t* out)
 // dst[t] = src[pos[t]] (t < n)
 int launch_gather_i32(hipStream_t s, int64_t n, const int64_t* pos, const int32_t* src,
                       int32_t* dst);
+// dst[t] = src[pos[t]] (t < n), fp64
+int launch_gather_f64(hipStream_t s, int64_t n, const int32_t* pos, const double* src,
+                      double* dst);
 int launch_validate_ids(hipStream_t s, int64_t n, const int32_t* ids, int32_t lo,
                         int32_t hi, int* bad);
 
@@ -332,5 +338,12 @@ template <typename TV, typename TIn>
 int build_csr(hipStream_t s, int64_t n, int64_t E, const int32_t* d_key,
               int32_t key_base, const int32_t* d_other, const TIn* d_val, int64_t* off,
               int32_t* idx, TV* val);
+
+// Rows of a CSR matrix stably sorted by first column (empty rows last):
+// perm[i] = original row of new row i; (rp2, ci2, v2) = the matrix in that
+// row order (rp2 has rows + 1 entries).
+int sort_rows_by_first_col(hipStream_t s, int64_t rows, int64_t cols, const int64_t* rp,
+                           const int32_t* ci, const double* v, int32_t* perm, int64_t* rp2,
+                           int32_t* ci2, double* v2);
 
 }  // namespace mr

@@ -156,9 +156,10 @@ def attach_peer_scalars(ctx, rank, world):
     """Switch ``ctx``'s CG scalars to the peer all-reduce (include/mr_als.h
     ``mr_als_set_peer``): every rank exports its exchange buffer's IPC handle,
     ``torch.distributed`` gathers the handles in rank order, every rank maps
-    its peers'.  Collective: all ranks call it.  Returns True on success;
-    on any rank's failure every rank keeps its collective scalars (the
-    outcome is agreed by an all-reduce first)."""
+    its peers', and one self-test reduction checks the sums.  Collective: all
+    ranks call it.  Returns True on success; on any rank's failure every rank
+    keeps its collective scalars (each step's outcome is agreed by an
+    all-reduce)."""
     import torch
     import torch.distributed as dist
     L = _lib.lib()
@@ -169,14 +170,21 @@ def attach_peer_scalars(ctx, rank, world):
     if any(h is None for h in handles):
         return False
     joined = ctypes.create_string_buffer(b"".join(handles), 64 * world)
-    ok = L.mr_als_set_peer(ctx._h, joined, int(rank), int(world)) == 0
-    flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
-    if dist.get_backend() == "nccl":
-        flag = flag.cuda()
-    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-    if int(flag.item()) != 1:
-        raise RuntimeError("peer scalar all-reduce could not be set up on every rank: "
-                           + _lib.last_error())
+
+    def agree(ok):
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        if dist.get_backend() == "nccl":
+            flag = flag.cuda()
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        return int(flag.item()) == 1
+
+    if not agree(L.mr_als_set_peer(ctx._h, joined, int(rank), int(world)) == 0):
+        L.mr_als_set_peer(ctx._h, None, int(rank), 0)
+        return False
+    # one reduction through the mapped buffers on every rank before trusting them
+    if not agree(L.mr_als_peer_selftest(ctx._h) == 0):
+        L.mr_als_set_peer(ctx._h, None, int(rank), 0)
+        return False
     ctx._peer = joined
     return True
 
@@ -201,6 +209,5 @@ def sharded_context(user_ids, item_ids, ratings, k, num_users, num_items, device
     else:
         ctx.set_comm(comm.struct, ub, ib)
         ctx._comm_owner = comm
-    if scalars == "peer":
-        attach_peer_scalars(ctx, rank, world)
+    ctx.peer_scalars = scalars == "peer" and attach_peer_scalars(ctx, rank, world)
     return ctx

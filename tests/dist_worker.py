@@ -102,6 +102,8 @@ def engine_sharded(d, max_iteration, rank, world, mode, skew=False):
     bounds = (skewed_bounds(nU, world), skewed_bounds(nI, world)) if skew else None
     ctx = sharded_context(d["user_ids"], d["item_ids"], d["ratings"], k, nU, nI, dev, comm,
                           bounds=bounds, scalars="peer" if mode == "engine_peer" else "collective")
+    if mode == "engine_peer" and not ctx.peer_scalars:
+        raise RuntimeError("peer scalar all-reduce was not set up (self-test failed)")
     ctx.set_factors(d["U0"], d["V0"])
     ret = ctx.run(0.01, max_iteration)
     U, V = ctx.get_factors()

@@ -42,10 +42,10 @@ def test_cg_goldens_through_reference_abi(gpu, name):
     sibling seed its stop moved by one iteration.  So: the iteration count
     within one of the reference's (at any recorded thread count) -- equal
     where the reference's is thread-count invariant and its rr before the
-    stop is stable --, x within 1e-8 of the oracle's restatement (pinned to
-    the reference at 1e-12) run for the GPU's own iteration count, and, at
-    the reference's count, x within max(1e-9, 20 x its thread-count spread)
-    and final rr within 1e-6 relative."""
+    stop is stable: then also x within 1e-8 of the oracle's restatement
+    (pinned to the reference at 1e-12) and within max(1e-9, 20 x the
+    reference's thread-count spread) of its x, final rr within 1e-6 relative;
+    otherwise the stop by rr < 1e-6 and x within 2e-4 of the reference's."""
     d = load_golden(name)
     tol = max(1e-9, 20 * float(d["tc_spread"])) if "tc_spread" in d else 1e-9
     its_ref = [int(d["iterations"])] + [int(i) for i in d.get("iterations_by_tc", [])]
@@ -57,14 +57,18 @@ def test_cg_goldens_through_reference_abi(gpu, name):
               f"{float(d['final_rr']):.4e}", flush=True)
         if stable:
             assert it == int(d["iterations"]), (name, it, its_ref)
-        else:
-            assert min(its_ref) - 1 <= it <= max(its_ref) + 1, (name, it, its_ref)
-        xo, ito, _ = O.cg_least_squares(d["row_ptr"], d["col_idx"], d["vals"], int(d["ncols"]),
-                                        d["b"], d["x0"], 0.01, it)
-        assert rel_err(x, xo) <= 1e-8, (name, rel_err(x, xo))
-        if it == int(d["iterations"]):
+            xo, ito, _ = O.cg_least_squares(d["row_ptr"], d["col_idx"], d["vals"],
+                                            int(d["ncols"]), d["b"], d["x0"], 0.01, it)
+            assert rel_err(x, xo) <= 1e-8, (name, rel_err(x, xo))
             assert rel_err(x, d["x"]) <= tol, (name, rel_err(x, d["x"]))
             assert abs(rr - float(d["final_rr"])) <= 1e-6 * max(1.0, float(d["final_rr"]))
+        else:
+            # the late iterations are chaotic: permuting A's rows in the oracle
+            # alone (a summation-order change) moves x after 35 iterations by
+            # 7e-5 and rr by 30x; the converged solutions agree to ~1e-8
+            assert min(its_ref) - 1 <= it <= max(its_ref) + 1, (name, it, its_ref)
+            assert rr < 1e-6 and float(d["final_rr"]) < 1e-6
+            assert rel_err(x, d["x"]) <= 2e-4, (name, rel_err(x, d["x"]))
 
 
 @pytest.mark.parametrize("max_it", [0, 1, 2, 3, 7])
