@@ -62,7 +62,8 @@ def load_data(shape, k, cache_dir="/tmp"):
     return rs
 
 
-def algorithmic_cost(cls, k, n_users, n_items, n_ratings, ldk, fused=True, n_ratings_items=None):
+def algorithmic_cost(cls, k, n_users, n_items, n_ratings, ldk, fused=True, n_ratings_items=None,
+                     onepass=True):
     """(bytes, flops) per launch of a kernel class; definitions in DESIGN.md.
 
     Normal equations are stored "tri16" (mr_internal.h): the nb(nb-1)/2
@@ -76,19 +77,24 @@ def algorithmic_cost(cls, k, n_users, n_items, n_ratings, ldk, fused=True, n_rat
     would put a symmetric kernel above the MFMA peak.  The kernel's executed
     MFMA work is nb(nb+1)/2 * 512 flop per rating (diagonal blocks full).
     With the fused CG start (default) the Gram launch also reads x and writes
-    r, p, q.  CG vectors r / p / q are fp64 (8 B), x and G fp32 (4 B)."""
+    r, p, q.  CG vectors r / p / q are fp64 (8 B), x and G fp32 (4 B).  The
+    one-pass CG iteration (default) makes the matvec launch also apply the
+    previous iteration's x / r update: per vector entry it reads p, r, q, x
+    and writes p, r, q, x (6 x 8 + 2 x 4 B) instead of p rw, r read, q write
+    (4 x 8 B); cg_update then only runs the finish pass once per solve."""
     K = k + 1
     nb = (k + 15) // 16
     gsz = (nb * (nb - 1) // 2 + nb // 2 + nb % 2) * 256 + (nb // 2) * 16
     n_ri = n_ratings if n_ratings_items is None else n_ratings_items   # item-view ratings
+    vb = 6 * 8 + 2 * 4 if onepass else 4 * 8     # vector bytes per entry and launch
     if cls == "matvec_users":
         E = n_users
         g = E * (gsz + ldk + 1) * 4               # G_e blocks + Gs row + count
-        v = E * (ldk + 1) * 8 * 4                 # p read+write, r read, Ap write (fp64)
+        v = E * (ldk + 1) * vb
         return g + v, E * 2.0 * K * K
     if cls == "matvec_items":
         E = n_items
-        return E * gsz * 4 + E * ldk * 8 * 4, E * 2.0 * k * k
+        return E * gsz * 4 + E * ldk * vb, E * 2.0 * k * k
     if cls == "gram_users":
         # per rating: (idx, value) 8 B + gathered item row k*4 B; output blocks
         b = n_ratings * (8 + 4 * k) + n_users * (gsz + 2 * ldk + 2) * 4
@@ -230,6 +236,8 @@ def main():
     ap.add_argument("--solver", default="cg", choices=["cg", "cholesky"])
     ap.add_argument("--ridge", type=float, default=0.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-onepass", action="store_true",
+                    help="CG iteration as matvec + update (two kernels) instead of one pass")
     ap.add_argument("--no-fuse-start", action="store_true",
                     help="start CG with a matvec + update pass instead of the Gram epilogue")
     ap.add_argument("--no-kernel-events", action="store_true",
@@ -316,6 +324,8 @@ def main():
         ctx.set_factors(U0, V0)
     if args.no_fuse_start:
         ctx.set_option("fuse_start", 0)
+    if args.no_onepass:
+        ctx.set_option("cg_onepass", 0)
     if args.cg_speculate is not None:
         ctx.set_option("cg_speculate", args.cg_speculate)
     ctx.sync()
@@ -394,8 +404,11 @@ def main():
     avg_s = tot_ms / launches / 1e3
     _, nU, _ = ctx.local_size("users")
     _, nI, n_local_items = ctx.local_size("items")
+    # one-pass CG: unsharded or with peer scalars (RCCL collectives: two kernels)
+    onepass = (not args.no_onepass and k <= 128
+               and (dist is None or getattr(ctx, "peer_scalars", False)))
     nbytes, nflops = algorithmic_cost(cls, k, nU, nI, n_local_users, ldk, not args.no_fuse_start,
-                                      n_local_items)
+                                      n_local_items, onepass)
     bound = "mfma" if cls.startswith("gram") and k >= 32 else "hbm"
     if bound == "hbm":
         achieved, peak, unit = nbytes / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
@@ -422,7 +435,7 @@ def main():
         n = st["kernel_launches"][c]
         if n:
             b, fl = algorithmic_cost(c, k, nU, nI, n_local_users, ldk, not args.no_fuse_start,
-                                     n_local_items)
+                                     n_local_items, onepass)
             kernel_table[c] = {"total_ms": round(ms, 3), "launches": n,
                                "avg_us": round(ms / n * 1e3, 2),
                                "alg_GBps": round(b / (ms / n / 1e3) / 1e9, 1) if b else None,
@@ -451,7 +464,8 @@ def main():
                    "parallelism": (f"shard{world}" if world > 1 or args.force_shard
                                    else "single"),
                    "cg_scalars": ("peer all-reduce (IPC)" if getattr(ctx, "peer_scalars", False)
-                                  else "rccl all-reduce" if dist is not None else "local")},
+                                  else "rccl all-reduce" if dist is not None else "local"),
+                   "cg_iteration": "one pass" if onepass else "matvec + update"},
         "roofline": {"kernel": cls, "bound": bound, "achieved": round(achieved, 2),
                      "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
                      "traffic": traffic,

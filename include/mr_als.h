@@ -159,8 +159,13 @@ int mr_als_set_timing(mr_als* ctx, int enable);
  *                         the solve stopped exits at once: results identical)
  *   MR_OPT_WAIT_TIMEOUT_S host wait for a published CG state, seconds
  *                         (default 300; a stalled peer rank then fails the
- *                         call instead of hanging it) */
-enum { MR_OPT_FUSE_START = 0, MR_OPT_CG_SPECULATE = 1, MR_OPT_WAIT_TIMEOUT_S = 2 };
+ *                         call instead of hanging it)
+ *   MR_OPT_CG_ONEPASS     1 (default): one kernel per CG iteration (the
+ *                         previous iteration's x / r update deferred into
+ *                         the next matvec, r'.r' from r.r, r.q, q.q; k <= 128,
+ *                         unsharded or peer scalars); 0: matvec + update */
+enum { MR_OPT_FUSE_START = 0, MR_OPT_CG_SPECULATE = 1, MR_OPT_WAIT_TIMEOUT_S = 2,
+       MR_OPT_CG_ONEPASS = 3 };
 int mr_als_set_option(mr_als* ctx, int option, double value);
 /* Ratings per Gram work item: heavier entities are split across waves and
  * their partial normal equations combined in order.  Applies to contexts

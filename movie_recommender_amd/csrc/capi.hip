@@ -277,6 +277,7 @@ int mr_als_set_option(mr_als* ctx, int option, double value) {
   MR_CHECK(ctx, "null context");
   switch (option) {
     case MR_OPT_FUSE_START: ctx->eng.fuse_start = value != 0.0; return 0;
+    case MR_OPT_CG_ONEPASS: ctx->eng.onepass = value != 0.0; return 0;
     case MR_OPT_CG_SPECULATE:
       // every rank of a sharded run must use the same level (it decides which
       // launches, and with them which collectives, are issued)

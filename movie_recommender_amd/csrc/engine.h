@@ -78,6 +78,7 @@ struct Engine {
   double ridge = 0.0;
   int chunk = 2048;
   bool fuse_start = true;   // CG start in the Gram epilogue (MR_OPT_FUSE_START)
+  bool onepass = true;      // one kernel per CG iteration (MR_OPT_CG_ONEPASS)
   int speculate = 1;        // 0: never enqueue ahead; 1: enqueue t+2 while t+1 runs when
                             // state t proves t+1 cannot stop; 2: always one ahead
                             // when t provably cannot stop (MR_OPT_CG_SPECULATE;
@@ -135,6 +136,7 @@ struct Engine {
   int gram(Side& S, bool start = false);
   int x_ptrs(Side& S, float** xf, float** xb);
   int cg(Side& S, double min_dec, int max_it, double* final_rr, bool started = false);
+  int cg_onepass(Side& S, double min_dec, int max_it, double* final_rr, bool started);
   CgStart cg_start_of(Side& S);
   int solve(Side& S);
   int half_step(bool user, double min_dec, int max_it, double* final_rr);

@@ -291,9 +291,9 @@ int Engine::build_side(Side& S, bool user, int64_t n, const int32_t* d_key,
     MR_HIP(hipMemsetAsync(S.pb, 0, S.E * sizeof(double), stream));
     MR_HIP(hipMemsetAsync(S.qb, 0, S.E * sizeof(double), stream));
   }
-  // fused CG start: one (r.r, p.Gp) pair per Gram block, then per split block
+  // fused CG start: one (r.r, p.Gp, q.q) triple per Gram block, then per split block
   S.n_start_pairs = gram_blocks(S.n_work) + (S.n_split + 3) / 4;
-  if (dalloc(&S.start_parts, 2 * std::max<int64_t>(1, S.n_start_pairs), stream)) return -1;
+  if (dalloc(&S.start_parts, 3 * std::max<int64_t>(1, S.n_start_pairs), stream)) return -1;
   // matvec grid: one wave per entity, fixed grid for reproducible partials
   int64_t g = (S.E + 3) / 4;
   S.n_part_mv = (int)std::max<int64_t>(1, std::min<int64_t>(g, kMaxParts));
@@ -324,7 +324,7 @@ int Engine::init(int dev, int k_, int64_t U_, int64_t I_, int64_t n_u,
                        hipHostMallocMapped | hipHostMallocCoherent));
   memset(h_mirror, 0, kMirrorSlots * sizeof(CgMirror));
   MR_HIP(hipHostGetDevicePointer((void**)&d_mirror, h_mirror, 0));
-  if (dalloc(&d_state, 1, stream) || dalloc(&partials, kMaxParts, stream) ||
+  if (dalloc(&d_state, 1, stream) || dalloc(&partials, 3 * kMaxParts, stream) ||
       dalloc(&d_flag, 4, stream))
     return -1;
   su.e0 = u0; su.E = u1 - u0;
@@ -771,6 +771,8 @@ int Engine::x_ptrs(Side& S, float** xf, float** xb) {
 // that t cannot terminate (fails == 0, rr far above 1e-6, t+1 < max_it) --
 // so the stream stays busy without launching iterations that would be idle.
 int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr, bool started) {
+  if (onepass && k <= kMaxK && (!sharded() || peer_on))
+    return cg_onepass(S, min_dec, max_it, final_rr, started);
   float *xf, *xb;
   x_ptrs(S, &xf, &xb);
   const bool user = S.user;
@@ -803,7 +805,7 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr, bool start
       const CgStart cs = cg_start_of(S);
       if (tic(MR_K_CG_START, -1, &a)) return -1;
       if (launch_cg_start_split(stream, user, k, S.split, S.n_split, direct_dst(S), cs,
-                                S.start_parts + 2 * gram_blocks(S.n_work)))
+                                S.start_parts + 3 * gram_blocks(S.n_work)))
         return -1;
       if (toc(MR_K_CG_START, -1, a)) return -1;
     }
@@ -927,6 +929,111 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr, bool start
   }
   for (size_t i = pend0; i < pending.size(); ++i) pending[i].n_real = ms.n_matvec;
   MR_CHECK(ms.ret >= 0, "peer all-reduce of the CG scalars timed out (a rank did not arrive)");
+  if (final_rr) *final_rr = ms.final_rr;
+  return ms.ret;
+}
+
+// One-pass CG (DESIGN.md "One-pass CG iteration"): the same solve as cg()
+// with ONE kernel per CG iteration (cg_onepass_kernel: the previous
+// iteration's deferred x / r update, p, q = G p and the three sums whose last
+// block takes alpha, r'.r' and the BETA rule, and publishes) and a finish
+// launch that applies the last iteration's update after the stop.  The
+// state after iteration t is published by kernel t (by the CG_START control
+// for t = 0 after a fused start); launch decisions follow exact published
+// states as in cg().  Unsharded, or sharded with the peer all-reduce (every
+// reduction happens in a last block, so ranks issue identical launches).
+int Engine::cg_onepass(Side& S, double min_dec, int max_it, double* final_rr, bool started) {
+  float *xf, *xb;
+  x_ptrs(S, &xf, &xb);
+  const bool user = S.user;
+  const int mv_cls = user ? MR_K_MATVEC_USERS : MR_K_MATVEC_ITEMS;
+  const int64_t n = S.E * ldk;
+  const int64_t nb = user ? S.E : 0;
+  const size_t pend0 = pending.size();
+  memset(h_init, 0, sizeof(CgState));
+  h_init->min_dec = min_dec;
+  h_init->max_it = max_it;
+  h_init->peer = peer_on ? d_peer : nullptr;
+  h_init->onepass = 1;
+  hipEvent_t a = nullptr;
+  std::vector<int> seq_of;   // publish seq of the state after iteration t
+  int launched = 0;          // iteration kernels enqueued (t = 0 .. launched-1)
+  CgMirror ms{};
+  if (started) {
+    if (S.n_split) {
+      const CgStart cs = cg_start_of(S);
+      if (tic(MR_K_CG_START, -1, &a)) return -1;
+      if (launch_cg_start_split(stream, user, k, S.split, S.n_split, direct_dst(S), cs,
+                                S.start_parts + 3 * gram_blocks(S.n_work)))
+        return -1;
+      if (toc(MR_K_CG_START, -1, a)) return -1;
+    }
+    // INIT rule, alpha_0 and iteration 0's BETA step (its update deferred)
+    seq_of.push_back(++mirror_seq);
+    if (tic(MR_K_CG_CONTROL, -1, &a)) return -1;
+    if (launch_cg_control(stream, d_state, CG_START, CTL_BOTH, S.start_parts,
+                          (int)S.n_start_pairs, d_mirror, seq_of[0], min_dec, max_it, 2))
+      return -1;
+    if (toc(MR_K_CG_CONTROL, -1, a)) return -1;
+    launched = 1;
+  } else {
+    MR_HIP(hipMemcpyAsync(d_state, h_init, sizeof(CgState), hipMemcpyHostToDevice, stream));
+    // r0 = G x - c ; p0 = -r0 ; rr (matrix.cpp:464-485), as in cg()
+    if (launch_x_to_vec(stream, n, nb, xf, xb, S.p, S.pb)) return -1;
+    if (tic(mv_cls, -1, &a)) return -1;
+    if (launch_cg_matvec(stream, user, d_state, 0, S.E, k, S.G, S.Gs, S.Gn, S.p, S.pb, S.r,
+                         S.rb, S.q, S.qb, partials, S.n_part_mv))
+      return -1;
+    if (toc(mv_cls, -1, a)) return -1;
+    const int seq_init = ++mirror_seq;
+    if (tic(MR_K_CG_UPDATE, -1, &a)) return -1;
+    if (launch_cg_update(stream, d_state, UPD_INIT, n, nb, xf, S.r, S.p, S.q, S.C, xb, S.rb,
+                         S.pb, S.qb, S.Cb, partials, kUpdParts, d_state, d_mirror, seq_init))
+      return -1;
+    if (toc(MR_K_CG_UPDATE, -1, a)) return -1;
+    if (wait_mirror(seq_init, &ms)) return -1;
+    MR_CHECK(ms.ret >= 0, "peer all-reduce of the CG scalars timed out (a rank did not arrive)");
+  }
+  auto launch_iter = [&](int t) -> int {
+    seq_of.push_back(++mirror_seq);
+    hipEvent_t ev = nullptr;
+    if (tic(mv_cls, t, &ev)) return -1;
+    if (launch_cg_onepass(stream, user, d_state, t > 0 ? 1 : 0, S.E, k, S.G, S.Gs, S.Gn, S.p,
+                          S.pb, S.r, S.rb, S.q, S.qb, xf, xb, partials, S.n_part_mv, d_mirror,
+                          seq_of.back()))
+      return -1;
+    return toc(mv_cls, t, ev);
+  };
+  auto enqueue_to = [&](int nt) -> int {   // iterations 0 .. nt-1 enqueued
+    while (launched < std::min(nt, max_it))
+      if (launch_iter(launched++)) return -1;
+    return 0;
+  };
+  const int spec = speculate;
+  int known = -1;   // ms = the exact state after iteration `known`
+  if (started || !ms.done) {
+    while (true) {
+      // iteration known+1 is what publishes the next state; with the state
+      // after `known` proving known+1 cannot stop, known+2 goes out too
+      int ahead = known + 2;
+      if (spec && known >= 0 && known + 2 < max_it &&
+          (spec >= 2 || (ms.fails == 0 && ms.rr > 1e-4)))
+        ahead = known + 3;
+      if (enqueue_to(ahead)) return -1;
+      MR_CHECK(known + 1 < (int)seq_of.size(), "CG did not terminate");
+      if (wait_mirror(seq_of[known + 1], &ms)) return -1;
+      ++known;
+      MR_CHECK(ms.ret >= 0, "peer all-reduce of the CG scalars timed out (a rank did not arrive)");
+      if (ms.done) break;
+    }
+  }
+  // the stopped iteration's x / r update (pending flag checked on the device)
+  if (tic(MR_K_CG_UPDATE, -1, &a)) return -1;
+  if (launch_cg_update(stream, d_state, UPD_FINISH, n, nb, xf, S.r, S.p, S.q, S.C, xb, S.rb,
+                       S.pb, S.qb, S.Cb, partials, kUpdParts))
+    return -1;
+  if (toc(MR_K_CG_UPDATE, -1, a)) return -1;
+  for (size_t i = pend0; i < pending.size(); ++i) pending[i].n_real = ms.n_matvec;
   if (final_rr) *final_rr = ms.final_rr;
   return ms.ret;
 }

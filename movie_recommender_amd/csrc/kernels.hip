@@ -268,14 +268,16 @@ __device__ __forceinline__ void tile_matvec(
 // CG start for ONE entity, by one wave, in block form (cg_least_squares,
 // matrix.cpp:464-476 and the first matvec / dot of its loop, :493-497):
 //   r0 = G x - c,  p0 = -r0,  q0 = G p0
-// written to the (fp64) CG vectors; this wave's lanes add r0.r0 to drr and
-// p0.q0 to dpq (callers reduce in a fixed order).  G / Gs / Gn / C / Cb hold
+// written to the (fp64) CG vectors; this wave's lanes add r0.r0 to drr,
+// p0.q0 to dpq and q0.q0 to dqq (callers reduce in a fixed order; the
+// one-pass CG derives r1.r1 from them, r0.q0 being exactly -p0.q0).  G / Gs / Gn / C / Cb hold
 // the entity's finished normal equations (after slab_reduce for split
 // entities).
 template <int NB, bool USER>
 __device__ __forceinline__ void cg_start_entity(int64_t e, int k, int ldk,
                                                 const GramDst& D, const CgStart& cs,
-                                                MvScratch<NB>& sc, double& drr, double& dpq) {
+                                                MvScratch<NB>& sc, double& drr, double& dpq,
+                                                double& dqq) {
   constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2, NTILE = NO + NF + (NB & 1);
   constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
   const int lane = threadIdx.x & 63;
@@ -339,6 +341,7 @@ __device__ __forceinline__ void cg_start_entity(int64_t e, int k, int ldk,
   // q0 = G p0 and p0.q0 (:493-497)
   tile_matvec<NB, USER>(g, sc, pb, Gs_e, gn, k, yo, yb);
   d = 0.0;
+  double dq = 0.0;
 #pragma unroll
   for (int h = 0; h < NV; ++h) {
     const int o = lane + 64 * h;
@@ -347,34 +350,42 @@ __device__ __forceinline__ void cg_start_entity(int64_t e, int k, int ldk,
       if (n < k) {
         cs.q[e * ldk + n] = yo[h];
         d = fma(yo[h], sc.pv[o], d);
+        dq = fma(yo[h], yo[h], dq);
       }
     }
   }
   if (USER && lane == 0) {
     cs.qb[e] = yb;
     d = fma(yb, pb, d);
+    dq = fma(yb, yb, dq);
   }
   dpq += wave_sum_f64(d);
+  dqq += wave_sum_f64(dq);
   __builtin_amdgcn_wave_barrier();
 }
 
-// Fixed-order (r.r, p.Gp) pair per block: wave partials summed in wave order.
-__device__ __forceinline__ void store_start_pair(double drr, double dpq, double* parts) {
-  __shared__ double shp[4][2];
+// Fixed-order (r.r, p.Gp, q.q) triple per block: wave partials summed in wave
+// order.
+__device__ __forceinline__ void store_start_sums(double drr, double dpq, double dqq,
+                                                 double* parts) {
+  __shared__ double shp[4][3];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   if (lane == 0) {
     shp[wid][0] = drr;
     shp[wid][1] = dpq;
+    shp[wid][2] = dqq;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    double a = 0.0, b = 0.0;
+    double a = 0.0, b = 0.0, c = 0.0;
     for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
       a += shp[w][0];
       b += shp[w][1];
+      c += shp[w][2];
     }
-    parts[2 * (int64_t)blockIdx.x] = a;
-    parts[2 * (int64_t)blockIdx.x + 1] = b;
+    parts[3 * (int64_t)blockIdx.x] = a;
+    parts[3 * (int64_t)blockIdx.x + 1] = b;
+    parts[3 * (int64_t)blockIdx.x + 2] = c;
   }
 }
 
@@ -497,8 +508,8 @@ __device__ __forceinline__ void acc_matvec(const floatx4 (&acc)[NB * (NB + 1) / 
 // Fused CG start of one unsplit entity from the Gram wave's registers
 // (cg_least_squares, matrix.cpp:464-476 and iteration 0's matvec / dot,
 // :493-497, in block form): r0 = G x - c, p0 = -r0, q0 = G p0, written to
-// the fp64 CG vectors; adds r0.r0 to drr and p0.q0 to dpq (lane partials
-// summed across the wave).  cacc / sacc: c and the row sums at virtual
+// the fp64 CG vectors; adds r0.r0 to drr, p0.q0 to dpq and q0.q0 to dqq
+// (lane partials summed across the wave).  cacc / sacc: c and the row sums at virtual
 // (b, col) in every lane (already reduced over q); wt / gn: user-side
 // sum of ratings and count; xv / xb: x at virtual (b, col) and its bias.
 template <int NB, bool USER>
@@ -507,7 +518,7 @@ __device__ __forceinline__ void start_from_acc(const floatx4 (&acc)[NB * (NB + 1
                                                float wt, float gn, const float (&xv)[NB],
                                                float xb, int64_t e, int k, int ldk,
                                                const CgStart& cs, StartScratch<NB>& sc,
-                                               double& drr, double& dpq) {
+                                               double& drr, double& dpq, double& dqq) {
   constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
   const int lane = threadIdx.x & 63, q = lane >> 4, col = lane & 15;
   if (q == 0) {
@@ -568,6 +579,7 @@ __device__ __forceinline__ void start_from_acc(const floatx4 (&acc)[NB * (NB + 1
   acc_matvec<NB>(acc, sc, k, yo);
   d = 0.0;
   ybp = 0.0;
+  double dq = 0.0;
 #pragma unroll
   for (int h = 0; h < NV; ++h) {
     const int o = lane + 64 * h;
@@ -582,6 +594,7 @@ __device__ __forceinline__ void start_from_acc(const floatx4 (&acc)[NB * (NB + 1
         }
         cs.q[e * ldk + n] = y;
         d = fma(y, pn[h], d);
+        dq = fma(y, y, dq);
       }
     }
   }
@@ -590,9 +603,11 @@ __device__ __forceinline__ void start_from_acc(const floatx4 (&acc)[NB * (NB + 1
     if (lane == 0) {
       cs.qb[e] = qb;
       d = fma(qb, pb, d);
+      dq = fma(qb, qb, dq);
     }
   }
   dpq += wave_sum_f64(d);
+  dqq += wave_sum_f64(dq);
 }
 
 // ---------------------------------------------------------------------------
@@ -794,7 +809,7 @@ __device__ __forceinline__ void gram_wave(
     const int32_t* __restrict__ idx, const float* __restrict__ val,
     const float* __restrict__ F, const float* __restrict__ bias, int k, int ldk, int zrow,
     const GramDst& direct, const GramDst& slab, const CgStart& cs, StartScratch<NB>* ssc,
-    double& drr, double& dpq) {
+    double& drr, double& dpq, double& dqq) {
   constexpr int T = NB * (NB + 1) / 2;
   const int lane = threadIdx.x & 63;
   // work-item fields in SGPRs: all control flow below is scalar
@@ -956,7 +971,7 @@ __device__ __forceinline__ void gram_wave(
   if constexpr (FUSE) {
     if (!to_slab)
       start_from_acc<NB, USER>(acc, cacc, sacc, wt, (float)wlen, xv, xbv, went, k, ldk, cs,
-                               *ssc, drr, dpq);
+                               *ssc, drr, dpq, dqq);
   }
 }
 
@@ -972,17 +987,17 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 3 : 1)) void gram_kernel(
     GramDst direct, GramDst slab, CgStart cs) {
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t wi = (int64_t)blockIdx.x * GRAM_WAVES + wid;
-  double drr = 0.0, dpq = 0.0;
+  double drr = 0.0, dpq = 0.0, dqq = 0.0;
   if constexpr (!FUSE) {
     if (wi >= n_work) return;
     gram_wave<NB, USER, false, BUF>(wi, work, idx, val, F, bias, k, ldk, zrow, direct, slab, cs,
-                                    nullptr, drr, dpq);
+                                    nullptr, drr, dpq, dqq);
   } else {
     __shared__ StartScratch<NB> scr[GRAM_WAVES];
     if (wi < n_work)
       gram_wave<NB, USER, true, BUF>(wi, work, idx, val, F, bias, k, ldk, zrow, direct, slab,
-                                     cs, &scr[wid], drr, dpq);
-    store_start_pair(drr, dpq, cs.parts);
+                                     cs, &scr[wid], drr, dpq, dqq);
+    store_start_sums(drr, dpq, dqq, cs.parts);
   }
 }
 
@@ -995,9 +1010,10 @@ __global__ __launch_bounds__(256) void cg_start_split_kernel(const SplitItem* __
   __shared__ MvScratch<NB> scr[4];
   const int wid = threadIdx.x >> 6;
   const int64_t i = (int64_t)blockIdx.x * 4 + wid;
-  double drr = 0.0, dpq = 0.0;
-  if (i < n_split) cg_start_entity<NB, USER>(split[i].entity, k, ldk, direct, cs, scr[wid], drr, dpq);
-  store_start_pair(drr, dpq, parts);
+  double drr = 0.0, dpq = 0.0, dqq = 0.0;
+  if (i < n_split)
+    cg_start_entity<NB, USER>(split[i].entity, k, ldk, direct, cs, scr[wid], drr, dpq, dqq);
+  store_start_sums(drr, dpq, dqq, parts);
 }
 
 template <int NB>
@@ -1543,7 +1559,7 @@ __device__ __forceinline__ void apply_beta(CgScalars& v, double rr2) {
   }
 }
 
-// Peer all-reduce of `count` (<= 2) doubles by ONE thread (the finalizing
+// Peer all-reduce of `count` (<= 3) doubles by ONE thread (the finalizing
 // thread of a kernel whose blocks have all finished): write this rank's
 // values into its record of every rank's exchange buffer, tag it with the
 // reduction's sequence number (release, system scope), wait for the tags of
@@ -1567,7 +1583,7 @@ __device__ bool peer_sum(PeerComm* pc, double* vals, int count) {
     __hip_atomic_store(reinterpret_cast<uint64_t*>(rec + 3), (uint64_t)s, __ATOMIC_RELEASE,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  double acc[2] = {0.0, 0.0};
+  double acc[3] = {0.0, 0.0, 0.0};
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
   for (int q = 0; q < world; ++q) {
     const double* rec = pc->buf[rank] + (slot * world + q) * 4;
@@ -1834,6 +1850,210 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 4 : 2)) void cg_matvec_kernel(
   }
 }
 
+// One-pass CG iteration (DESIGN.md "One-pass CG iteration"): ONE kernel per
+// CG iteration t >= 1 instead of matvec + update.  Each wave first applies,
+// for its entity, iteration t-1's deferred update (x += alpha p, r += alpha q:
+// matrix.cpp:501-503, the same fp64 expressions as cg_update_kernel), then
+// p = -r + beta p (:521), q = G p, and adds p.q, r.q and q.q to its partials.
+// The last-arriving block sums them in a fixed order and takes iteration t's
+// scalars: alpha = r.r / p.q (:497) and, without a second pass over the
+// vectors, r'.r' = r.r + 2 alpha r.q + alpha^2 q.q for the new residual
+// r' = r + alpha q -- the same quantity as the reference's direct r'.r'
+// (:507) up to rounding of order eps r.r / r'.r' (CG's per-iteration decrease
+// is moderate, see the design note) -- then the BETA rule and the publish.
+// Iteration t's own update is deferred to kernel t+1 or, after the stop, to
+// cg_update_kernel(UPD_FINISH).  `update` = 0 for t = 0 of an unfused start
+// (nothing deferred yet).  Per vector entry: read p, r, q, x; write p, r, q, x
+// (56 B fp64/fp32) against 72 B for matvec + update, and one kernel boundary
+// less per iteration.
+template <int NB, bool USER>
+__global__ __launch_bounds__(256, (NB <= 4 ? 4 : 2)) void cg_onepass_kernel(
+    CgState* __restrict__ st, int update, int64_t E, int k, int ldk,
+    const float* __restrict__ G, const float* __restrict__ Gs, const float* __restrict__ Gn,
+    double* __restrict__ p, double* __restrict__ pb, double* __restrict__ r,
+    double* __restrict__ rb, double* __restrict__ q, double* __restrict__ qb,
+    float* __restrict__ x, float* __restrict__ xb, double* __restrict__ partials,
+    CgMirror* mirror, int seq) {
+  if (ald(&st->done)) return;
+  const double beta = ald(&st->beta), alpha = ald(&st->alpha);
+  constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2, NTILE = NO + NF + (NB & 1);
+  constexpr int64_t GS = (int64_t)NTILE * 256 + NF * 16;   // == gsize_of(k)
+  constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
+  __shared__ MvScratch<NB> scr[MV_WAVES];
+  __shared__ double rvs[MV_WAVES][16 * NB];
+  __shared__ double sh[MV_WAVES];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  MvScratch<NB>& sc = scr[wid];
+  double* rs = rvs[wid];
+  double dpq = 0.0, drq = 0.0, dqq = 0.0;
+  for (int64_t e = (int64_t)blockIdx.x * MV_WAVES + wid; e < E;
+       e += (int64_t)gridDim.x * MV_WAVES) {
+    double* pe = p + e * ldk;
+    double* re = r + e * ldk;
+    double* qe = q + e * ldk;
+    float* xe = x + e * ldk;
+    double pi[NV], ri[NV], qi[NV];
+    float xi[NV];
+#pragma unroll
+    for (int h = 0; h < NV; ++h) {
+      const int i = lane + 64 * h;
+      pi[h] = (i < NP) ? pe[i] : 0.0;
+      ri[h] = (i < NP) ? re[i] : 0.0;
+      qi[h] = (update && i < NP) ? qe[i] : 0.0;
+      xi[h] = (update && i < NP) ? xe[i] : 0.f;
+    }
+    double pbias = 0.0, rbias = 0.0, qbias = 0.0;
+    float xbias = 0.f;
+    if (USER) {
+      pbias = pb[e];
+      rbias = rb[e];
+      if (update) {
+        qbias = qb[e];
+        xbias = xb[e];
+      }
+    }
+    const floatx4* __restrict__ Ge = reinterpret_cast<const floatx4*>(G + e * GS);
+    float4 g[NTILE];
+#pragma unroll
+    for (int t = 0; t < NTILE; ++t) {
+      const floatx4 v4 = __builtin_nontemporal_load(Ge + t * 64 + lane);
+      g[t] = make_float4(v4[0], v4[1], v4[2], v4[3]);
+    }
+    float d2 = 0.f;
+    if (NF > 0 && lane < 16 * NF) d2 = G[e * GS + NTILE * 256 + lane];
+#pragma unroll
+    for (int h = 0; h < NV; ++h) {
+      const int i = lane + 64 * h;
+      if (i < NP) {
+        double rn = ri[h], pn = pi[h];
+        if (update) {
+          rn = fma(alpha, qi[h], ri[h]);
+          re[i] = rn;
+          xe[i] = (float)fma(alpha, pi[h], (double)xi[h]);
+          pn = fma(beta, pi[h], -rn);
+          pe[i] = pn;
+        }
+        sc.pv[virt_of(i, NB)] = pn;
+        rs[virt_of(i, NB)] = rn;
+      }
+    }
+    if (USER && update) {
+      const double rbn = fma(alpha, qbias, rbias);
+      const double pbn = fma(beta, pbias, -rbn);
+      if (lane == 0) {
+        rb[e] = rbn;
+        xb[e] = (float)fma(alpha, pbias, (double)xbias);
+        pb[e] = pbn;
+      }
+      rbias = rbn;
+      pbias = pbn;
+    }
+    if (NF > 0 && lane < 16 * NF) sc.dd[lane] = d2;
+    __builtin_amdgcn_wave_barrier();
+    double yo[NV], ybv = 0.0;
+    tile_matvec<NB, USER>(g, sc, pbias, USER ? Gs + e * ldk : nullptr, USER ? Gn[e] : 0.f, k, yo,
+                          ybv);
+    double a = 0.0, b = 0.0, c = 0.0;
+#pragma unroll
+    for (int h = 0; h < NV; ++h) {
+      const int o = lane + 64 * h;
+      if (o < NP) {
+        const int n = nat_of(o, NB);
+        if (n < k) {
+          qe[n] = yo[h];
+          a = fma(yo[h], sc.pv[o], a);
+          b = fma(yo[h], rs[o], b);
+          c = fma(yo[h], yo[h], c);
+        }
+      }
+    }
+    if (USER && lane == 0) {
+      qb[e] = ybv;
+      a = fma(ybv, pbias, a);
+      b = fma(ybv, rbias, b);
+      c = fma(ybv, ybv, c);
+    }
+    dpq += wave_sum_f64(a);
+    drq += wave_sum_f64(b);
+    dqq += wave_sum_f64(c);
+    __builtin_amdgcn_wave_barrier();
+  }
+  const int64_t np = gridDim.x;
+  double tot[3];
+  tot[0] = block_sum_f64<256>(lane == 0 ? dpq : 0.0, sh);
+  __syncthreads();
+  tot[1] = block_sum_f64<256>(lane == 0 ? drq : 0.0, sh);
+  __syncthreads();
+  tot[2] = block_sum_f64<256>(lane == 0 ? dqq : 0.0, sh);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      __hip_atomic_store(&partials[j * np + blockIdx.x], tot[j], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // last-arriving block: iteration t's scalars (see last_block_finalize for
+  // the memory-model basis of this hand-off)
+  __shared__ int s_last;
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_last = __hip_atomic_fetch_add(&st->arrive, 1u, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  double sum[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x)
+      acc += __hip_atomic_load(&partials[j * np + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sum[j] = block_sum_f64<256>(acc, sh);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(&st->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (PeerComm* pc = ald(&st->peer)) {
+      if (!peer_sum(pc, sum, 3)) {
+        peer_fail(st, mirror, seq);
+        return;
+      }
+    }
+    CgScalars v = load_state(st);
+    const double al = v.rr / sum[0];
+    v.alpha = al;
+    v.n_matvec += 1;
+    apply_beta(v, fma(al * al, sum[2], fma(2.0 * al, sum[1], v.rr)));
+    store_state(st, v);
+    ast(&st->pending, 1);
+    publish(v, mirror, seq);
+  }
+}
+
+int launch_cg_onepass(hipStream_t s, bool user_side, CgState* st, int update, int64_t E, int k,
+                      const float* G, const float* Gs, const float* Gn, double* p, double* pb,
+                      double* r, double* rb, double* q, double* qb, float* x, float* xb,
+                      double* partials, int n_part, CgMirror* mirror, int seq) {
+  if (n_part <= 0) return 0;
+#define MR_OP_CASE(NB)                                                                      \
+  case NB:                                                                                  \
+    if (user_side)                                                                          \
+      MR_LAUNCH((cg_onepass_kernel<NB, true>), dim3(n_part), dim3(256), 0, s, st, update, E, \
+                k, ldk_of(k), G, Gs, Gn, p, pb, r, rb, q, qb, x, xb, partials, mirror, seq); \
+    else                                                                                    \
+      MR_LAUNCH((cg_onepass_kernel<NB, false>), dim3(n_part), dim3(256), 0, s, st, update,  \
+                E, k, ldk_of(k), G, Gs, Gn, p, pb, r, rb, q, qb, x, xb, partials, mirror,  \
+                seq);                                                                       \
+    break;
+  switch (nb16_of(k)) {
+    MR_OP_CASE(1) MR_OP_CASE(2) MR_OP_CASE(3) MR_OP_CASE(4)
+    MR_OP_CASE(5) MR_OP_CASE(6) MR_OP_CASE(7) MR_OP_CASE(8)
+    default: set_error("one-pass CG needs k <= 128"); return -1;
+  }
+#undef MR_OP_CASE
+  MR_HIP(hipGetLastError());
+  return 0;
+}
+
 // K2 for k > 128: the same block GEMV (fused p update, fp64 products, p.q
 // partial, control in the last block) with the tiles streamed from memory
 // instead of held in registers: one wave per entity, two passes over the
@@ -2030,7 +2250,8 @@ __global__ __launch_bounds__(256) void cg_update_kernel(
     float* __restrict__ xb, double* __restrict__ rb, double* __restrict__ pb,
     const double* __restrict__ qb, const float* __restrict__ cb,
     double* __restrict__ partials, CgState* fst, CgMirror* mirror, int seq) {
-  if (ald(&st->done)) return;
+  // UPD_FINISH (one-pass CG): the stopped solve's deferred last update, if any
+  if (mode == UPD_FINISH ? !ald(&st->pending) : ald(&st->done) != 0) return;
   __shared__ double sh[4];
   // sharded runs: alpha = rr / (all-reduced p.Ap), the ALPHA rule inline
   const double alpha = ald(&st->sharded) && mode != UPD_INIT ? ald(&st->rr) / ald(&st->comm[0])
@@ -2093,6 +2314,7 @@ __global__ __launch_bounds__(256) void cg_update_kernel(
       acc = fma(rv, rv, acc);
     }
   }
+  if (mode == UPD_FINISH) return;
   const double tot = block_sum_f64<256>(acc, sh);
   if (fst) store_partial(partials, tot);
   else if (threadIdx.x == 0) partials[blockIdx.x] = tot;
@@ -2143,38 +2365,42 @@ __global__ __launch_bounds__(CTL_THREADS) void cg_control_kernel(
   __shared__ double sh[CTL_THREADS / 64];
   if (ctl & CTL_REDUCE) {
     if (phase == CG_START) {
-      // (r.r, p.Gp) pairs (one per Gram block: ~E/4 of them, written by
-      // every XCD): thread t sums pairs t, t + T, t + 2T, ... in order, 8
-      // coalesced loads in flight, then the fixed-order block tree.
-      const double2* pp = reinterpret_cast<const double2*>(partials);
-      double a = 0.0, b = 0.0;
+      // (r.r, p.Gp, q.q) triples (one per Gram block: ~E/4 of them, written
+      // by every XCD): thread t sums triples t, t + T, t + 2T, ... in order,
+      // 8 loads in flight, then the fixed-order block tree.
+      double a = 0.0, b = 0.0, c = 0.0;
       for (int base = 0; base < n_part; base += 8 * CTL_THREADS) {
-        double2 v[8];
+        double v[8][3];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int i = base + j * CTL_THREADS + threadIdx.x;
-          v[j] = (i < n_part) ? pp[i] : make_double2(0.0, 0.0);
+#pragma unroll
+          for (int m = 0; m < 3; ++m) v[j][m] = (i < n_part) ? partials[3 * (int64_t)i + m] : 0.0;
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          a += v[j].x;
-          b += v[j].y;
+          a += v[j][0];
+          b += v[j][1];
+          c += v[j][2];
         }
       }
       const double ta = block_sum_f64<CTL_THREADS>(a, sh);
       __syncthreads();
       const double tb = block_sum_f64<CTL_THREADS>(b, sh);
+      __syncthreads();
+      const double tc = block_sum_f64<CTL_THREADS>(c, sh);
       if (threadIdx.x == 0) {
-        double t2[2] = {ta, tb};
+        double t3[3] = {ta, tb, tc};
         PeerComm* pc = ald(&st->peer);
-        if (pc && (ctl & CTL_FINALIZE) && !peer_sum(pc, t2, 2)) {
+        if (pc && (ctl & CTL_FINALIZE) && !peer_sum(pc, t3, 3)) {
           ast(&st->comm[0], 0.0);
           ast(&st->comm[1], 0.0);
           peer_fail(st, mirror, seq);
           return;
         }
-        ast(&st->comm[0], t2[0]);
-        ast(&st->comm[1], t2[1]);
+        ast(&st->comm[0], t3[0]);
+        ast(&st->comm[1], t3[1]);
+        ast(&st->comm[2], t3[2]);
       }
     } else {
       double acc = 0.0;
@@ -2189,9 +2415,11 @@ __global__ __launch_bounds__(CTL_THREADS) void cg_control_kernel(
     // unless that ended the solve, alpha of iteration 0 from p0.G p0
     CgScalars v;
     const double rr = ald(&st->comm[0]), pq = ald(&st->comm[1]);
+    const int onepass = (sharded >> 1) & 1;   // bit 1 of the argument
     v.min_dec = min_dec;
     v.max_it = max_it;
-    v.sharded = sharded;
+    v.sharded = sharded & 1;
+    ast(&st->onepass, onepass);
     v.n_matvec = 0;
     v.alpha = 0.0;
     v.beta = 0.0;
@@ -2209,6 +2437,16 @@ __global__ __launch_bounds__(CTL_THREADS) void cg_control_kernel(
       v.n_matvec = 1;    // the fused iteration-0 matvec
     }
     ast(&st->arrive, 0u);
+    ast(&st->pending, 0);
+    if (onepass && !v.done) {
+      // one-pass CG: iteration 0's BETA step now, from r1.r1 = r0.r0 +
+      // 2 alpha r0.q0 + alpha^2 q0.q0 with r0.q0 = -p0.q0 (p0 = -r0 exactly);
+      // its x / r update is applied by iteration 1's kernel (or the finish)
+      const double qq = ald(&st->comm[2]);
+      const double a = v.alpha;
+      apply_beta(v, fma(a * a, qq, fma(-2.0 * a, pq, rr)));
+      ast(&st->pending, 1);
+    }
     store_state(st, v);
     publish(v, mirror, seq);
     return;

@@ -198,7 +198,7 @@ struct CgState {
   double beta;
   double final_rr;
   double min_dec;   // min_r_decrease
-  double comm[2];   // local sums exchanged by all-reduce in sharded runs
+  double comm[3];   // local sums exchanged by all-reduce in sharded runs
   int32_t it;       // iteration counter
   int32_t fails;    // consecutive beta > 1 - min_dec
   int32_t done;     // solve finished: every later kernel is a no-op
@@ -209,6 +209,9 @@ struct CgState {
   int32_t sharded;  // 1: the last block only sums into comm[0] for the all-reduce
   PeerComm* peer;   // non-null: the finalizing thread all-reduces its sum with
                     // the peers itself (no collective launches; rules as unsharded)
+  int32_t onepass;  // one kernel per CG iteration (cg_matvec_kernel, DESIGN.md
+                    // "One-pass CG iteration"); set by the host per solve
+  int32_t pending;  // one-pass: the last iteration's x / r update is not applied yet
 };
 
 // Host-visible copies of the CG state: a ring of kMirrorSlots records in
@@ -232,7 +235,7 @@ struct CgMirror {
 // control kernel also (re)initialises the state from its arguments.
 enum CgPhase { CG_INIT = 0, CG_ALPHA = 1, CG_BETA = 2, CG_START = 3 };
 enum CgCtl { CTL_REDUCE = 1, CTL_FINALIZE = 2, CTL_BOTH = 3 };
-enum CgUpd { UPD_INIT = 0, UPD_STEP = 1 };
+enum CgUpd { UPD_INIT = 0, UPD_STEP = 1, UPD_FINISH = 2 };
 
 // Kernel launchers (kernels.hip) ---------------------------------------------
 // F has zrow+1 rows; row zrow (and bias[zrow]) is all zero.
@@ -262,7 +265,16 @@ int launch_cg_matvec(hipStream_t s, bool user_side, const CgState* st,
                      const double* r, const double* rb, double* y, double* yb,
                      double* partials, int n_part, CgState* fst = nullptr,
                      int phase = CG_INIT, CgMirror* mirror = nullptr, int beta_seq = 0);
+// One-pass CG iteration (kernels.hip cg_onepass_kernel): the previous
+// iteration's deferred x / r update (update != 0), p = -r + beta p, q = G p,
+// p.q / r.q / q.q partials (3 x n_part doubles in partials) and, in the last
+// block, alpha, r'.r', the BETA rule and the publish under `seq`.  k <= 128.
+int launch_cg_onepass(hipStream_t s, bool user_side, CgState* st, int update, int64_t E, int k,
+                      const float* G, const float* Gs, const float* Gn, double* p, double* pb,
+                      double* r, double* rb, double* q, double* qb, float* x, float* xb,
+                      double* partials, int n_part, CgMirror* mirror, int seq);
 // x is the fp32 factor table (and bias), r / p / q the fp64 CG vectors.
+// mode UPD_FINISH: apply a one-pass solve's pending last update (no sums).
 int launch_cg_update(hipStream_t s, const CgState* st, int mode, int64_t n,
                      int64_t nb, float* x, double* r, double* p, const double* q,
                      const float* c, float* xb, double* rb, double* pb,

@@ -12,7 +12,8 @@ import numpy as np
 from . import _lib
 
 SOLVERS = {"cg": 0, "cholesky": 1}
-OPTIONS = {"fuse_start": 0, "cg_speculate": 1, "wait_timeout_s": 2}   # include/mr_als.h
+OPTIONS = {"fuse_start": 0, "cg_speculate": 1, "wait_timeout_s": 2,
+           "cg_onepass": 3}   # include/mr_als.h
 
 
 def _i32(a):

@@ -91,7 +91,7 @@ def skewed_bounds(n, world):
     return b
 
 
-def engine_sharded(d, max_iteration, rank, world, mode, skew=False):
+def engine_sharded(d, max_iteration, rank, world, mode, skew=False, onepass=1):
     import torch.distributed as dist
     from movie_recommender_amd.distributed import TorchComm, sharded_context
     from movie_recommender_amd.engine import device_count
@@ -104,6 +104,7 @@ def engine_sharded(d, max_iteration, rank, world, mode, skew=False):
                           bounds=bounds, scalars="peer" if mode == "engine_peer" else "collective")
     if mode == "engine_peer" and not ctx.peer_scalars:
         raise RuntimeError("peer scalar all-reduce was not set up (self-test failed)")
+    ctx.set_option("cg_onepass", onepass)
     ctx.set_factors(d["U0"], d["V0"])
     ret = ctx.run(0.01, max_iteration)
     U, V = ctx.get_factors()
@@ -145,6 +146,7 @@ def main():
     ap.add_argument("--max-iteration", type=int, default=200)
     ap.add_argument("--out", required=True)
     ap.add_argument("--skew", action="store_true", help="uneven shard boundaries")
+    ap.add_argument("--onepass", type=int, default=1, help="engine option cg_onepass")
     a = ap.parse_args()
     import torch.distributed as dist
     dist.init_process_group("gloo")
@@ -156,7 +158,7 @@ def main():
     elif a.mode == "oracle":
         U, V, ret = oracle_sharded(d, a.max_iteration, rank, world)
     else:
-        U, V, ret = engine_sharded(d, a.max_iteration, rank, world, a.mode, a.skew)
+        U, V, ret = engine_sharded(d, a.max_iteration, rank, world, a.mode, a.skew, a.onepass)
     if rank == 0:
         np.savez(a.out, U=U, V=V, ret=ret)
     dist.barrier()

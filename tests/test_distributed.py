@@ -22,13 +22,15 @@ def free_port():
     return p
 
 
-def run_workers(mode, fixture, nproc, tmp_path, max_iteration=200, timeout=600, skew=False):
-    out = str(tmp_path / f"{mode}_{nproc}{'_skew' if skew else ''}.npz")
+def run_workers(mode, fixture, nproc, tmp_path, max_iteration=200, timeout=600, skew=False,
+                onepass=1):
+    out = str(tmp_path / f"{mode}_{nproc}{'_skew' if skew else ''}_op{onepass}.npz")
     env = dict(os.environ, OMP_NUM_THREADS="2", MR_QUIET="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1",
            f"--master-port={free_port()}", WORKER, "--mode", mode, "--fixture", fixture,
-           "--max-iteration", str(max_iteration), "--out", out] + (["--skew"] if skew else [])
+           "--max-iteration", str(max_iteration), "--out", out, "--onepass", str(onepass)] + \
+        (["--skew"] if skew else [])
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env,
                        cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
@@ -180,6 +182,7 @@ def test_engine_rccl_path_matches_single(gpu, tmp_path):
     nproc = max(1, min(2, gpu.mr_device_count()))
     U, V, ret = run_workers("engine_rccl", fixture, nproc, tmp_path)
     with AlsContext(d["user_ids"], d["item_ids"], d["ratings"], 32, 200, 150) as ctx:
+        ctx.set_option("cg_onepass", 0)   # the RCCL collectives run the two-kernel CG
         ctx.set_factors(d["U0"], d["V0"])
         ret1 = ctx.run()
         U1, V1 = ctx.get_factors()
@@ -279,11 +282,20 @@ def test_engine_peer_scalars_match_collective(gpu, tmp_path, fixture, max_it, np
     sum of two terms is the same in either order), at world 3 within the
     reference tolerance; both against the compiled reference's golden."""
     d = load_golden(fixture)
-    Up, Vp, retp = run_workers("engine_peer", fixture, nproc, tmp_path, max_it, skew=skew)
-    Ug, Vg, retg = run_workers("engine_gloo", fixture, nproc, tmp_path, max_it, skew=skew)
+    # the two-kernel CG (cg_onepass 0) with either transport of the scalars
+    Up, Vp, retp = run_workers("engine_peer", fixture, nproc, tmp_path, max_it, skew=skew,
+                               onepass=0)
+    Ug, Vg, retg = run_workers("engine_gloo", fixture, nproc, tmp_path, max_it, skew=skew,
+                               onepass=0)
     assert retp == retg == int(d["ret"])
     if nproc == 2:
         assert np.array_equal(Up, Ug) and np.array_equal(Vp, Vg)
     else:
         assert rel_err(Up, Ug) < 1e-5 and rel_err(Vp, Vg) < 1e-5
     assert rel_err(Up, d["U"]) < 1e-5 and rel_err(Vp, d["V"]) < 1e-5
+    # the one-pass CG (the default with peer scalars: one reduction of three
+    # sums per CG iteration) against the golden
+    U1, V1, ret1 = run_workers("engine_peer", fixture, nproc, tmp_path, max_it, skew=skew,
+                               onepass=1)
+    assert ret1 == int(d["ret"])
+    assert rel_err(U1, d["U"]) < 1e-5 and rel_err(V1, d["V"]) < 1e-5

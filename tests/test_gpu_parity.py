@@ -91,14 +91,16 @@ def test_als_mlshape_golden(gpu, name):
 
 
 @pytest.mark.parametrize("name", HEADLINE)
-@pytest.mark.parametrize("chunk,fuse", [(2048, 1), (64, 1), (2048, 0)])
-def test_headline_paths_golden(gpu, name, chunk, fuse):
+@pytest.mark.parametrize("chunk,fuse,onepass", [(2048, 1, 1), (64, 1, 1), (2048, 0, 1),
+                                                (2048, 1, 0), (64, 1, 0), (2048, 0, 0)])
+def test_headline_paths_golden(gpu, name, chunk, fuse, onepass):
     """Every CG start path against the compiled reference at k = 32 / 64 /
     128: the Gram-epilogue start (fuse 1), the start of split entities after
     slab_reduce (chunk 64 splits every entity), and the unfused reference
-    order (fuse 0: x -> matvec -> INIT update).  Every launch-ahead level
-    (MR_OPT_CG_SPECULATE 0, 1, 2) must give identical CG counts and
-    bitwise-identical factors."""
+    order (fuse 0: x -> matvec -> INIT update); each with the one-pass CG
+    iteration (cg_onepass 1, the default) and with matvec + update (0).
+    Every launch-ahead level (MR_OPT_CG_SPECULATE 0, 1, 2) must give
+    identical CG counts and bitwise-identical factors."""
     from movie_recommender_amd.engine import AlsContext
     from movie_recommender_amd import _lib
     d = load_golden(name)
@@ -111,6 +113,7 @@ def test_headline_paths_golden(gpu, name, chunk, fuse):
                             gram_chunk=chunk) as ctx:
                 ctx.set_option("fuse_start", fuse)
                 ctx.set_option("cg_speculate", spec)
+                ctx.set_option("cg_onepass", onepass)
                 ctx.set_factors(d["U0"], d["V0"])
                 ret = ctx.run(0.01, mi)
                 st = ctx.stats()
@@ -264,14 +267,16 @@ def test_gram_kernel_vs_numpy(gpu, k):
 
 
 @pytest.mark.parametrize("k", [5, 10, 32, 33, 64, 65, 128, 144, 200, 300])
-@pytest.mark.parametrize("fuse,chunk", [(1, 2048), (1, 64), (0, 2048)])
-def test_cg_iterations_vs_oracle(gpu, k, fuse, chunk):
+@pytest.mark.parametrize("fuse,chunk,onepass", [(1, 2048, 1), (1, 64, 1), (0, 2048, 1),
+                                                (1, 2048, 0), (0, 2048, 0)])
+def test_cg_iterations_vs_oracle(gpu, k, fuse, chunk, onepass):
     """The first CG iterations of both sides -- CG start (fused in the Gram
     epilogue, after slab_reduce for split entities, or the unfused matvec +
     INIT update), the NB = 1..8 block GEMV, the update and the fused control
     -- against the oracle's fp64 CG (matrix.cpp:456-529 in block form) run on
     the GPU's own normal equations (fp32 values read back).  What remains is
-    summation order: final rr within 1e-10, x within 2 fp32 ulps."""
+    summation order (and, one-pass, r'.r' from r.r + 2 alpha r.q + alpha^2
+    q.q): final rr within 1e-10, x within 2 fp32 ulps."""
     from movie_recommender_amd.engine import AlsContext
     from movie_recommender_amd import _lib
     from oracle import als_oracle as O
@@ -289,6 +294,7 @@ def test_cg_iterations_vs_oracle(gpu, k, fuse, chunk):
     try:
         with AlsContext(u, i, r, k, nU, nI, gram_chunk=chunk) as ctx:
             ctx.set_option("fuse_start", fuse)
+            ctx.set_option("cg_onepass", onepass)
             for side, nE in (("users", nU), ("items", nI)):
                 ctx.set_factors(U0, V0)
                 ctx.build_normal_equations(side)
@@ -405,11 +411,47 @@ def test_band_realistic_heldout_rmse(gpu):
     assert lo <= np.mean(vals) <= hi, (vals, lo, hi)
 
 
+def _gpu_rank_agreement(rs, U, V, k):
+    """The reference's quality metric on GPU-trained factors through the GPU
+    evaluation path (serving.MovieTable.evaluate = _als_eval +
+    compute_ranking_agreement, bit-exact against the reference's functions in
+    test_gpu_serving.py): every held-out user's raw ratings (residual +
+    median) against u[:k].v + u[k] + median.  Mean over users with an
+    agreement."""
+    from movie_recommender_amd.serving import MovieTable
+    ids = {i: i for i in range(rs.num_items)}
+    med = {i: float(rs.medians[i]) for i in range(rs.num_items)}
+    order = np.argsort(rs.test_user_ids, kind="stable")
+    tu = rs.test_user_ids[order]
+    ti = rs.test_item_ids[order]
+    raw = rs.test_ratings[order] + rs.medians[ti]
+    cuts = np.flatnonzero(np.diff(tu)) + 1
+    users = np.split(tu, cuts)
+    lists = [list(zip(a.tolist(), b.tolist())) for a, b in zip(np.split(ti, cuts),
+                                                              np.split(raw, cuts))]
+    table = MovieTable(k, V, ids, med)
+    try:
+        res = table.evaluate(U, [int(u[0]) for u in users], lists)
+    finally:
+        table.close()
+    a = res["agreement"]
+    return float(np.nanmean(a)), int(np.count_nonzero(~np.isnan(a)))
+
+
 def test_band_headline_shape_heldout_rmse(gpu):
-    """G4 at the headline shape: MovieLens-full-shaped synthetic data, k = 64,
-    4 ALS iterations; the mean held-out RMSE of 3 seeds must fall inside the
-    compiled reference's band (3 seeds x thread counts 4, 8; min - 3 sd ..
-    max + 3 sd), band_mlfull_k64.json from tests/golden/make_golden.py g8."""
+    """G4 at the headline shape (round 3): MovieLens-full-shaped synthetic
+    data, k = 64, 20 % of each user's ratings held out, the reference's loop
+    with max_iteration 4, initial factors from seeds 0..4 -- against 20 runs
+    of the compiled reference (the same 5 seeds x thread counts 1, 2, 4, 8;
+    band_mlfull_k64.json from tests/golden/make_golden.py g9).  The
+    reference is chaotic here (one seed's held-out RMSE moves 0.954 .. 1.007
+    between its own thread counts), so the GPU is one more "thread count" of
+    each seed: per seed, its held-out RMSE and its mean ranking agreement (the
+    reference's own quality metric, my_util.py:101-145, computed on the GPU)
+    must lie within that seed's reference range widened by 25 % of the
+    pooled range, and the 5-seed means within the pooled range.  The GPU
+    values are reported in a warning (kept in the pytest summary)."""
+    import warnings
     from movie_recommender_amd import synth
     from movie_recommender_amd.engine import AlsContext
     from oracle import als_oracle as O
@@ -420,19 +462,38 @@ def test_band_headline_shape_heldout_rmse(gpu):
     rs = synth.movielens_like(band["shape"], k, seed=band["data_seed"],
                               test_ratio=band["test_ratio"])
     assert rs.n == band["n_train"] and abs(float(np.sum(rs.ratings)) - band["ratings_checksum"]) < 1e-6
-    lo = band["test_rmse_min"] - 3 * band["test_rmse_std"]
-    hi = band["test_rmse_max"] + 3 * band["test_rmse_std"]
-    vals = []
-    for seed in range(3):
+    assert len(band["runs"]) >= 15
+    pool = {m: (min(r[m] for r in band["runs"]), max(r[m] for r in band["runs"]))
+            for m in ("test_rmse", "rank_agreement")}
+    got = {"test_rmse": [], "rank_agreement": [], "train_rmse": [], "ret": []}
+    report = []
+    for seed in sorted({r["seed"] for r in band["runs"]}):
         U0, V0 = init_factors(rs.num_users, rs.num_items, k, seed)
         with AlsContext(rs.user_ids, rs.item_ids, rs.ratings, k, rs.num_users,
                         rs.num_items) as ctx:
             ctx.set_factors(U0, V0)
-            ctx.run(0.01, mi)
+            ret = ctx.run(0.01, mi)
             U, V = ctx.get_factors()
-        vals.append(O.rmse(U, V, rs.test_user_ids, rs.test_item_ids, rs.test_ratings, k))
-        print(f"seed {seed}: held-out RMSE {vals[-1]:.5f} (band {lo:.5f} .. {hi:.5f})", flush=True)
-    assert lo <= np.mean(vals) <= hi, (vals, lo, hi)
+        vals = {"test_rmse": O.rmse(U, V, rs.test_user_ids, rs.test_item_ids, rs.test_ratings, k),
+                "train_rmse": O.rmse(U, V, rs.user_ids, rs.item_ids, rs.ratings, k),
+                "rank_agreement": _gpu_rank_agreement(rs, U, V, k)[0], "ret": ret}
+        for m in got:
+            got[m].append(vals[m])
+        runs = [r for r in band["runs"] if r["seed"] == seed]
+        line = (f"seed {seed}: GPU ret {ret} held-out RMSE {vals['test_rmse']:.5f} (reference "
+                f"{min(r['test_rmse'] for r in runs):.5f} .. {max(r['test_rmse'] for r in runs):.5f})"
+                f" agreement {vals['rank_agreement']:.5f} (reference "
+                f"{min(r['rank_agreement'] for r in runs):.5f} .. "
+                f"{max(r['rank_agreement'] for r in runs):.5f})")
+        print(line, flush=True)
+        report.append(line)
+        for m in ("test_rmse", "rank_agreement"):
+            lo, hi = min(r[m] for r in runs), max(r[m] for r in runs)
+            w = 0.25 * (pool[m][1] - pool[m][0])
+            assert lo - w <= vals[m] <= hi + w, (seed, m, vals[m], lo, hi)
+    warnings.warn("headline-shape band (k=64, 4 ALS iterations): " + "; ".join(report))
+    for m in ("test_rmse", "rank_agreement"):
+        assert pool[m][0] <= np.mean(got[m]) <= pool[m][1], (m, got[m], pool[m])
 
 
 def test_predict_matches_reference_formula(gpu):
