@@ -109,7 +109,9 @@ struct Engine {
            const int* uv_iid, const double* uv_r, int64_t n_i, const int* iv_uid,
            const int* iv_iid, const double* iv_r, int64_t u0, int64_t u1, int64_t i0,
            int64_t i1);
-  int place_chunks_by_xcd(Side& S, std::vector<WorkItem>& work, int64_t chunk);
+  int build_work_xcd(Side& S, const std::vector<int64_t>& off, int64_t chunk,
+                     std::vector<WorkItem>& work, std::vector<SplitItem>& split,
+                     int32_t& nslab, bool& applied);
   int build_side(Side& S, bool user, int64_t n, const int32_t* d_key,
                  const int32_t* d_other, const double* d_r);
   int set_factors(const double* hU, const double* hV);

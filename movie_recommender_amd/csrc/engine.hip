@@ -168,58 +168,96 @@ int Engine::resolve_timing() {
 // ----------------------------------------------------------------------------
 // construction
 // ----------------------------------------------------------------------------
-// XCD-aware placement of the heavy entities' chunks in the Gram work list.
-// Gram block b holds work items 4b .. 4b+3 and blocks are dealt round-robin
-// over the 8 XCDs (MI355X_MICROARCH.md), so the XCD of list position p is
-// (p / 4) mod 8.  A heavy entity's rating list is cut into full chunks of
-// `chunk` ratings; within an entity the ratings are ordered by opposite id
-// (the CSR build sorts stably, and the data arrive grouped by user), so a
-// chunk gathers opposite rows from a narrow id range.  The full chunks are
-// dealt to the chunk positions so that XCD x receives the x-th eighth of them
-// in opposite-id order (key = the id at the chunk's middle): each XCD's L2
-// then serves ~1/8 of the opposite table for this share of the gathers.
-// Bit-identical: every chunk keeps its ratings and its slab record (summed by
-// slab_reduce in chunk order), unsplit entities keep their positions (the
-// fused CG start's per-block partial sums), and chunk waves add nothing to
-// those sums -- only which CU runs which chunk changes.  Applied to the
-// matrix-core Gram (32 <= k <= 128, four work items per block) when the
-// opposite table exceeds 16 MiB (four XCDs' L2): ML-full k = 64 items side
-// (U, 26 MB) 606 -> 582 us same-box; the users side (V, 13 MB, ~60 % L2
-// hits already) measured no gain.
-int Engine::place_chunks_by_xcd(Side& S, std::vector<WorkItem>& work, int64_t chunk) {
+// Gram work list with XCD-aligned opposite-id ranges (round 3).  Gram block b
+// holds work items 4b .. 4b+3 and blocks are dealt round-robin over the 8
+// XCDs (MI355X_MICROARCH.md), so list position p runs on XCD (p / 4) mod 8.
+// Every heavy entity (more than `chunk` ratings) is cut at the opposite-id
+// boundaries x * n_other / 8 (its ratings are ordered by opposite id: the
+// CSR build sorts stably and ML-style input arrives grouped by user; an
+// entity whose list is not sorted keeps fixed-size chunks, labelled by their
+// middle id), each range into chunks of <= `chunk` ratings, and range x's
+// chunks are dealt to positions on XCD x: each XCD's L2 then holds 1/8 of
+// the opposite table (3.3 MB of U at k = 64) for the heavy entities'
+// gathers, instead of every XCD streaming all of it.  The chunks come first
+// (longest first within each XCD's queue; a queue that runs dry takes from
+// the fullest), then the unsplit entities heavy first.  A split entity's
+// partial records are summed by slab_reduce in range order, so its Gram sum
+// order differs from a plain 2048-rating cut (results change at rounding
+// level; tests/test_gpu_parity.py expected_layout restates this exactly).
+// Applied to the matrix-core Gram (32 <= k <= 128) when the opposite table
+// exceeds 16 MiB (ML-full k = 64: the items side, U = 26 MB); returns
+// applied = false otherwise.
+int Engine::build_work_xcd(Side& S, const std::vector<int64_t>& off, int64_t chunk,
+                           std::vector<WorkItem>& work, std::vector<SplitItem>& split,
+                           int32_t& nslab, bool& applied) {
   constexpr int64_t kWaves = 4, kXcds = 8;
-  const int64_t table = (S.user ? I : U) * (int64_t)ldk * 4;
+  applied = false;
+  const int64_t n_other = S.user ? I : U;
+  const int64_t table = n_other * (int64_t)ldk * 4;
   if (k < 32 || k > 128 || table <= ((int64_t)16 << 20)) return 0;
-  std::vector<int64_t> pos;
-  for (int64_t p = 0; p < (int64_t)work.size(); ++p)
-    if (work[p].slab >= 0 && work[p].len == chunk) pos.push_back(p);
-  const int64_t nc = (int64_t)pos.size();
-  if (nc < 2 * kWaves * kXcds) return 0;
-  std::vector<int64_t> mid(nc);
-  for (int64_t j = 0; j < nc; ++j) mid[j] = work[pos[j]].begin + work[pos[j]].len / 2;
-  int64_t* d_mid = nullptr;
-  int32_t* d_key = nullptr;
-  if (dalloc(&d_mid, nc, stream) || dalloc(&d_key, nc, stream)) return -1;
-  std::vector<int32_t> key(nc);
-  int rc = 0;
-  do {
-    if (t_stager.h2d(stream, d_mid, mid.data(), (size_t)nc * sizeof(int64_t))) { rc = -1; break; }
-    if (launch_gather_i32(stream, nc, d_mid, S.idx, d_key)) { rc = -1; break; }
-    if (t_stager.d2h(stream, key.data(), d_key, (size_t)nc * sizeof(int32_t))) { rc = -1; break; }
-  } while (0);
-  dfree(d_mid, stream);
-  dfree(d_key, stream);
-  if (rc) return rc;
-  std::vector<int64_t> by_key(nc), slots(pos);
-  for (int64_t j = 0; j < nc; ++j) by_key[j] = j;
-  std::stable_sort(by_key.begin(), by_key.end(),
-                   [&](int64_t a, int64_t b) { return key[a] < key[b]; });
-  std::stable_sort(slots.begin(), slots.end(), [&](int64_t a, int64_t b) {
-    return (a / kWaves) % kXcds < (b / kWaves) % kXcds;
-  });
-  std::vector<WorkItem> chunks(nc);
-  for (int64_t j = 0; j < nc; ++j) chunks[j] = work[pos[by_key[j]]];
-  for (int64_t j = 0; j < nc; ++j) work[slots[j]] = chunks[j];
+  bool any_heavy = false;
+  for (int64_t e = 0; e < S.E && !any_heavy; ++e) any_heavy = off[e + 1] - off[e] > chunk;
+  if (!any_heavy) return 0;
+  std::vector<int32_t> idx(S.nnz);
+  if (S.nnz) MR_D2H(idx.data(), S.idx, S.nnz * sizeof(int32_t), stream);
+  std::vector<std::vector<WorkItem>> q(kXcds);
+  std::vector<WorkItem> light;
+  for (int64_t e = 0; e < S.E; ++e) {
+    const int64_t b0 = off[e], b1 = off[e + 1], len = b1 - b0;
+    if (len <= chunk) {
+      light.push_back({b0, (int32_t)len, (int32_t)e, -1, 0});
+      continue;
+    }
+    const bool sorted = std::is_sorted(idx.begin() + b0, idx.begin() + b1);
+    const int32_t s0 = nslab;
+    auto cut = [&](int64_t a, int64_t z, int x) {   // [a, z) into chunks on XCD x
+      for (int64_t c = a; c < z; c += chunk) {
+        const int64_t l = std::min<int64_t>(chunk, z - c);
+        q[x].push_back({c, (int32_t)l, (int32_t)e, nslab++, 0});
+      }
+    };
+    if (sorted) {
+      int64_t a = b0;
+      for (int x = 0; x < kXcds; ++x) {
+        const int32_t hi = (int32_t)((x + 1) * n_other / kXcds);
+        const int64_t z = x == kXcds - 1 ? b1
+                                         : std::lower_bound(idx.begin() + a, idx.begin() + b1, hi) -
+                                               idx.begin();
+        cut(a, z, x);
+        a = z;
+      }
+    } else {
+      for (int64_t c = b0; c < b1; c += chunk) {
+        const int64_t l = std::min<int64_t>(chunk, b1 - c);
+        const int x = (int)std::min<int64_t>(kXcds - 1, idx[c + l / 2] * kXcds / n_other);
+        q[x].push_back({c, (int32_t)l, (int32_t)e, nslab++, 0});
+      }
+    }
+    split.push_back({(int32_t)e, s0, nslab - s0, 0});
+  }
+  int64_t n_chunks = 0;
+  for (auto& v : q) {
+    std::stable_sort(v.begin(), v.end(),
+                     [](const WorkItem& a, const WorkItem& b) { return a.len > b.len; });
+    n_chunks += (int64_t)v.size();
+  }
+  std::vector<size_t> head(kXcds, 0);
+  for (int64_t p = 0; p < n_chunks; ++p) {
+    int x = (int)((p / kWaves) % kXcds);
+    if (head[x] == q[x].size()) {   // this XCD's queue ran dry: the fullest one
+      size_t best = 0;
+      for (int y = 0; y < kXcds; ++y)
+        if (q[y].size() - head[y] > best) {
+          best = q[y].size() - head[y];
+          x = y;
+        }
+    }
+    work.push_back(q[x][head[x]++]);
+  }
+  std::stable_sort(light.begin(), light.end(),
+                   [](const WorkItem& a, const WorkItem& b) { return a.len > b.len; });
+  work.insert(work.end(), light.begin(), light.end());
+  applied = true;
   return 0;
 }
 
@@ -242,7 +280,9 @@ int Engine::build_side(Side& S, bool user, int64_t n, const int32_t* d_key,
   std::vector<SplitItem> split;
   work.reserve(S.E + n / chunk + 1);
   int32_t nslab = 0;
-  for (int64_t e = 0; e < S.E; ++e) {
+  bool xcd = false;
+  if (build_work_xcd(S, off, chunk, work, split, nslab, xcd)) return -1;
+  for (int64_t e = 0; e < (xcd ? 0 : S.E); ++e) {
     const int64_t len = off[e + 1] - off[e];
     if (len <= chunk) {
       work.push_back({off[e], (int32_t)len, (int32_t)e, -1, 0});
@@ -257,9 +297,9 @@ int Engine::build_side(Side& S, bool user, int64_t n, const int32_t* d_key,
       nslab += nc;
     }
   }
-  std::stable_sort(work.begin(), work.end(),
-                   [](const WorkItem& a, const WorkItem& b) { return a.len > b.len; });
-  if (place_chunks_by_xcd(S, work, chunk)) return -1;
+  if (!xcd)
+    std::stable_sort(work.begin(), work.end(),
+                     [](const WorkItem& a, const WorkItem& b) { return a.len > b.len; });
   S.n_work = (int64_t)work.size();
   S.n_split = (int64_t)split.size();
   S.n_slab = nslab;
@@ -327,6 +367,9 @@ int Engine::init(int dev, int k_, int64_t U_, int64_t I_, int64_t n_u,
   if (dalloc(&d_state, 1, stream) || dalloc(&partials, 3 * kMaxParts, stream) ||
       dalloc(&d_flag, 4, stream))
     return -1;
+  // every field defined before any kernel reads it: the fused CG start
+  // re-initialises the scalars but not `peer` (set only by set_peer)
+  MR_HIP(hipMemsetAsync(d_state, 0, sizeof(CgState), stream));
   su.e0 = u0; su.E = u1 - u0;
   si.e0 = i0; si.E = i1 - i0;
   // factor tables (replicated), zero padding columns

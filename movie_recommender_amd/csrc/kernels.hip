@@ -1866,8 +1866,14 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 4 : 2)) void cg_matvec_kernel(
 // (nothing deferred yet).  Per vector entry: read p, r, q, x; write p, r, q, x
 // (56 B fp64/fp32) against 72 B for matvec + update, and one kernel boundary
 // less per iteration.
+// Occupancy: 4 waves / SIMD (128 VGPRs) at NB <= 4 like cg_matvec_kernel,
+// except the user side at NB = 4, whose bias column needs a few registers
+// more than 128 (14 spilled registers at 4 waves): 3 waves / SIMD.
+#ifndef MR_OP_WAVES_U4
+#define MR_OP_WAVES_U4 3
+#endif
 template <int NB, bool USER>
-__global__ __launch_bounds__(256, (NB <= 4 ? 4 : 2)) void cg_onepass_kernel(
+__global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 : 4) : 2)) void cg_onepass_kernel(
     CgState* __restrict__ st, int update, int64_t E, int k, int ldk,
     const float* __restrict__ G, const float* __restrict__ Gs, const float* __restrict__ Gn,
     double* __restrict__ p, double* __restrict__ pb, double* __restrict__ r,
@@ -1882,10 +1888,11 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 4 : 2)) void cg_onepass_kernel(
   __shared__ MvScratch<NB> scr[MV_WAVES];
   __shared__ double rvs[MV_WAVES][16 * NB];
   __shared__ double sh[MV_WAVES];
+  __shared__ double wacc[MV_WAVES][3];   // the wave's running p.q, r.q, q.q (off the VGPRs)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   MvScratch<NB>& sc = scr[wid];
   double* rs = rvs[wid];
-  double dpq = 0.0, drq = 0.0, dqq = 0.0;
+  if (lane < 3) wacc[wid][lane] = 0.0;
   for (int64_t e = (int64_t)blockIdx.x * MV_WAVES + wid; e < E;
        e += (int64_t)gridDim.x * MV_WAVES) {
     double* pe = p + e * ldk;
@@ -1973,18 +1980,27 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 4 : 2)) void cg_onepass_kernel(
       b = fma(ybv, rbias, b);
       c = fma(ybv, ybv, c);
     }
-    dpq += wave_sum_f64(a);
-    drq += wave_sum_f64(b);
-    dqq += wave_sum_f64(c);
+    a = wave_sum_f64(a);
+    b = wave_sum_f64(b);
+    c = wave_sum_f64(c);
+    if (lane == 0) {
+      wacc[wid][0] += a;
+      wacc[wid][1] += b;
+      wacc[wid][2] += c;
+    }
     __builtin_amdgcn_wave_barrier();
   }
   const int64_t np = gridDim.x;
   double tot[3];
-  tot[0] = block_sum_f64<256>(lane == 0 ? dpq : 0.0, sh);
   __syncthreads();
-  tot[1] = block_sum_f64<256>(lane == 0 ? drq : 0.0, sh);
-  __syncthreads();
-  tot[2] = block_sum_f64<256>(lane == 0 ? dqq : 0.0, sh);
+  if (threadIdx.x == 0) {   // waves in order, as block_sum_f64 sums them
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      double t = 0.0;
+      for (int w = 0; w < MV_WAVES; ++w) t += wacc[w][j];
+      tot[j] = t;
+    }
+  }
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int j = 0; j < 3; ++j)

@@ -556,40 +556,75 @@ def test_full_size_gram_sampled(gpu):
         assert its >= 1 and np.isfinite(rr)
 
 
-def expected_layout(ids, other, ratings, E, chunk=2048, xcd_table_bytes=0):
-    """Host restatement of the context build: stable CSR by entity, then the
-    Gram work list (entities longer than `chunk` split into slabs numbered in
-    entity order; stable sort by length, heavy first) -- engine.hip build_side
-    -- and, when the opposite table exceeds 16 MiB, the XCD placement of the
-    full chunks (engine.hip place_chunks_by_xcd: chunks in order of the
-    opposite id at their middle, dealt to the chunk positions grouped by XCD
-    = (position // 4) % 8)."""
+def expected_layout(ids, other, ratings, E, chunk=2048, xcd_table_bytes=0, k=64, n_other=None):
+    """Host restatement of the context build (engine.hip build_side /
+    build_work_xcd): stable CSR by entity, then the Gram work list.  Plain:
+    entities longer than `chunk` split into slabs numbered in entity order,
+    stable sort by length, heavy first.  When the opposite table exceeds
+    16 MiB (32 <= k <= 128) and a heavy entity exists: every heavy entity cut
+    at the opposite-id boundaries x * n_other / 8 (fixed chunks labelled by
+    their middle id if its list is unsorted), each range into chunks of <=
+    `chunk`, range x's chunks dealt to positions p with (p // 4) % 8 == x
+    (queues longest first; a dry queue yields to the fullest), followed by
+    the unsplit entities heavy first."""
     order = np.argsort(ids, kind="stable")
     off = np.zeros(E + 1, np.int64)
     np.cumsum(np.bincount(ids, minlength=E), out=off[1:])
+    cidx = other[order].astype(np.int32)
+    lens = np.diff(off)
+    xcd = (xcd_table_bytes > (16 << 20) and 32 <= k <= 128 and bool(np.any(lens > chunk)))
     work = []
     nslab = 0
+    if not xcd:
+        for e in range(E):
+            ln = int(lens[e])
+            if ln <= chunk:
+                work.append((int(off[e]), ln, e, -1))
+            else:
+                nc = (ln + chunk - 1) // chunk
+                for c in range(nc):
+                    b = int(off[e]) + c * chunk
+                    work.append((b, min(chunk, int(off[e + 1]) - b), e, nslab + c))
+                nslab += nc
+        work.sort(key=lambda w: -w[1])     # stable: equal lengths keep entity order
+        return off, cidx, ratings[order].astype(np.float32), work
+    queues = [[] for _ in range(8)]
+    light = []
     for e in range(E):
-        ln = int(off[e + 1] - off[e])
-        if ln <= chunk:
-            work.append((int(off[e]), ln, e, -1))
+        b0, b1 = int(off[e]), int(off[e + 1])
+        if b1 - b0 <= chunk:
+            light.append((b0, b1 - b0, e, -1))
+            continue
+        seg = cidx[b0:b1]
+        if np.all(seg[1:] >= seg[:-1]):
+            a = b0
+            for x in range(8):
+                z = b1 if x == 7 else b0 + int(np.searchsorted(seg, (x + 1) * n_other // 8,
+                                                               side="left"))
+                for c in range(a, z, chunk):
+                    queues[x].append((c, min(chunk, z - c), e, nslab))
+                    nslab += 1
+                a = z
         else:
-            nc = (ln + chunk - 1) // chunk
-            for c in range(nc):
-                b = int(off[e]) + c * chunk
-                work.append((b, min(chunk, int(off[e + 1]) - b), e, nslab + c))
-            nslab += nc
-    work.sort(key=lambda w: -w[1])     # stable: equal lengths keep entity order
-    cidx = other[order].astype(np.int32)
-    pos = [p for p, w in enumerate(work) if w[3] >= 0 and w[1] == chunk]
-    if xcd_table_bytes > (16 << 20) and len(pos) >= 64:
-        key = [int(cidx[work[p][0] + work[p][1] // 2]) for p in pos]
-        by_key = sorted(range(len(pos)), key=lambda j: key[j])
-        slots = sorted(pos, key=lambda p: (p // 4) % 8)
-        chunks = [work[pos[j]] for j in by_key]
-        for j, sl in enumerate(slots):
-            work[sl] = chunks[j]
-    return off, cidx, ratings[order].astype(np.float32), work
+            for c in range(b0, b1, chunk):
+                ln = min(chunk, b1 - c)
+                x = min(7, int(cidx[c + ln // 2]) * 8 // n_other)
+                queues[x].append((c, ln, e, nslab))
+                nslab += 1
+    for qx in queues:
+        qx.sort(key=lambda w: -w[1])
+    head = [0] * 8
+    for p in range(sum(len(qx) for qx in queues)):
+        x = (p // 4) % 8
+        if head[x] == len(queues[x]):
+            best = 0
+            for y in range(8):
+                if len(queues[y]) - head[y] > best:
+                    best, x = len(queues[y]) - head[y], y
+        work.append(queues[x][head[x]])
+        head[x] += 1
+    light.sort(key=lambda w: -w[1])
+    return off, cidx, ratings[order].astype(np.float32), work + light
 
 
 def test_full_size_context_build_exact(gpu):
@@ -608,7 +643,8 @@ def test_full_size_context_build_exact(gpu):
             off, idx, val, (wb, wl, we, ws) = ctx.layout(side)
             n_other = rs.num_items if side == "users" else rs.num_users
             eoff, eidx, eval_, work = expected_layout(ids, other, rs.ratings, E,
-                                                      xcd_table_bytes=n_other * 64 * 4)
+                                                      xcd_table_bytes=n_other * 64 * 4, k=k,
+                                                      n_other=n_other)
             assert np.array_equal(off, eoff), side
             assert np.array_equal(idx, eidx), side
             assert np.array_equal(val, eval_), side

@@ -158,7 +158,8 @@ def test_c4_mlfull_k128_layout_and_gram(gpu, c4):
             n_other = rs.num_items if side == "users" else rs.num_users
             off, idx, val, (wb, wl, we, ws) = ctx.layout(side)
             eoff, eidx, eval_, work = expected_layout(ids, other, rs.ratings, E,
-                                                      xcd_table_bytes=n_other * k * 4)
+                                                      xcd_table_bytes=n_other * k * 4, k=k,
+                                                      n_other=n_other)
             assert np.array_equal(off, eoff) and np.array_equal(idx, eidx), side
             assert np.array_equal(val, eval_), side
             w = np.array(work, np.int64)

@@ -1,50 +1,74 @@
 """Host restatement of the Gram work list (engine.hip build_side +
-place_chunks_by_xcd), checked for the properties that make the XCD-aware chunk
-placement bit-identical: it only permutes the full chunks of split entities
-among their own slots, unsplit entities keep their positions (the fused CG
-start sums its per-block pairs by position), and XCD x = (slot // 4) % 8
-receives the x-th eighth of the chunks in opposite-id order.  The GPU test
-test_full_size_context_build_exact compares the device work list with the
-same restatement at the ML-full shape."""
+build_work_xcd), checked for the properties the XCD-aligned opposite-range cut
+relies on: every rating in exactly one work item, each heavy entity's
+partial records numbered consecutively in range order (slab_reduce sums them
+in that order), a chunk of range x gathers opposite rows only from
+[x n / 8, (x+1) n / 8) and sits on XCD x = (slot // 4) % 8 (a dry queue
+yields to the fullest), chunks before the unsplit entities, and small tables
+keep the plain layout.  The GPU tests test_full_size_context_build_exact and
+test_c4_mlfull_k128_layout_and_gram compare the device work list with the
+same restatement at full size."""
 import numpy as np
 
 from test_gpu_parity import expected_layout
 
 
-def _case(seed=0, n_ent=300, n_other=5000, chunk=64):
+def _case(seed=0, n_ent=300, n_other=5000, chunk=64, sorted_lists=True):
     rng = np.random.RandomState(seed)
     deg = np.minimum(rng.zipf(1.5, n_ent), 40 * chunk)
     ids = np.repeat(np.arange(n_ent), deg)
     other = np.concatenate([np.sort(rng.choice(n_other, d, replace=False)) for d in deg])
-    order = rng.permutation(len(ids))       # input order is not entity-major
+    # sorted_lists: input ordered by opposite id (as ML data ordered by user
+    # is for the items side); else a random input order
+    order = np.argsort(other, kind="stable") if sorted_lists else rng.permutation(len(ids))
     return ids[order].astype(np.int32), other[order].astype(np.int32), \
-        rng.uniform(1, 5, len(ids)), n_ent, chunk
+        rng.uniform(1, 5, len(ids)), n_ent, n_other, chunk
 
 
-def test_placement_is_a_slot_preserving_permutation():
-    ids, other, r, E, chunk = _case()
-    _, idx, _, base = expected_layout(ids, other, r, E, chunk=chunk)
-    _, _, _, placed = expected_layout(ids, other, r, E, chunk=chunk,
-                                      xcd_table_bytes=64 << 20)
-    assert sorted(base) == sorted(placed)
-    full = [p for p, w in enumerate(base) if w[3] >= 0 and w[1] == chunk]
-    assert len(full) >= 64
-    moved = [p for p in range(len(base)) if base[p] != placed[p]]
-    assert moved and set(moved) <= set(full)          # only full chunks move
-    assert all(placed[p][3] >= 0 and placed[p][1] == chunk for p in full)
-    # XCD groups in opposite-id order: max key of XCD x <= min key of XCD x+1
-    keys = {}
-    for p in full:
-        b, ln = placed[p][0], placed[p][1]
-        keys.setdefault((p // 4) % 8, []).append(int(idx[b + ln // 2]))
-    xs = sorted(keys)
-    for a, b in zip(xs, xs[1:]):
-        assert max(keys[a]) <= min(keys[b])
+def _check(ids, other, r, E, n_other, chunk):
+    off, idx, _, work = expected_layout(ids, other, r, E, chunk=chunk,
+                                        xcd_table_bytes=64 << 20, k=64, n_other=n_other)
+    cover = np.zeros(off[-1], np.int32)
+    for b, ln, e, s in work:
+        assert off[e] <= b and b + ln <= off[e + 1]
+        cover[b:b + ln] += 1
+    assert np.all(cover == 1)
+    n_chunks = sum(1 for w in work if w[3] >= 0)
+    assert all(w[3] >= 0 for w in work[:n_chunks]) and all(w[3] < 0 for w in work[n_chunks:])
+    light = [w[1] for w in work[n_chunks:]]
+    assert light == sorted(light, reverse=True)
+    slabs = {}
+    for b, ln, e, s in work[:n_chunks]:
+        slabs.setdefault(e, []).append((s, b))
+    for e, v in slabs.items():
+        v.sort()
+        assert [s for s, _ in v] == list(range(v[0][0], v[0][0] + len(v)))
+        assert [b for _, b in v] == sorted(b for _, b in v)     # range order = rating order
+    return off, idx, work, n_chunks
+
+
+def test_xcd_ranges_sorted_lists():
+    ids, other, r, E, n_other, chunk = _case()
+    off, idx, work, n_chunks = _check(ids, other, r, E, n_other, chunk)
+    assert n_chunks >= 64
+    on_home = 0
+    for p, (b, ln, e, s) in enumerate(work[:n_chunks]):
+        lo, hi = int(idx[b]), int(idx[b + ln - 1])
+        x = lo * 8 // n_other
+        assert hi * 8 // n_other == x            # one opposite range per chunk
+        on_home += (p // 4) % 8 == x
+    assert on_home >= 0.75 * n_chunks           # the rest: dry queues yielding
+
+
+def test_xcd_ranges_unsorted_lists_fall_back_to_fixed_chunks():
+    ids, other, r, E, n_other, chunk = _case(seed=2, sorted_lists=False)
+    off, idx, work, n_chunks = _check(ids, other, r, E, n_other, chunk)
+    assert all(ln == chunk or b + ln == off[e + 1] for b, ln, e, s in work[:n_chunks])
 
 
 def test_small_tables_are_not_placed():
-    ids, other, r, E, chunk = _case(seed=1)
+    ids, other, r, E, n_other, chunk = _case(seed=1)
     _, _, _, base = expected_layout(ids, other, r, E, chunk=chunk)
     _, _, _, same = expected_layout(ids, other, r, E, chunk=chunk,
-                                    xcd_table_bytes=16 << 20)
+                                    xcd_table_bytes=16 << 20, k=64, n_other=n_other)
     assert base == same

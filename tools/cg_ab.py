@@ -1,0 +1,55 @@
+"""A/B of the CG iteration at a FIXED number of CG iterations (no stop rule:
+min_r_decrease = -inf never fails, max_iteration = M), so summation-order
+changes cannot confound kernel timings.  ML-full shape, warmed up by a few
+ALS iterations; reports per side the solve time per CG iteration (HIP-event
+span of the solve phase / M) and the per-class kernel means.
+
+    python tools/cg_ab.py [--k 64] [--m 20] [--reps 3] [--onepass 0|1] [--tag NAME]
+(MR_LIB_PATH selects a variant library, tools/build_var.sh)"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from bench import load_data  # noqa: E402
+from movie_recommender_amd.engine import AlsContext  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--k", type=int, default=64)
+ap.add_argument("--m", type=int, default=20)
+ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--onepass", type=int, default=1)
+ap.add_argument("--tag", default="")
+a = ap.parse_args()
+rs = load_data("ml-full", a.k)
+rng = np.random.RandomState(0)
+U0 = rng.uniform(-1, 1, rs.num_users * (a.k + 1))
+V0 = rng.uniform(-1, 1, rs.num_items * a.k)
+out = {"tag": a.tag or os.environ.get("MR_LIB_PATH", "default"), "k": a.k, "m": a.m,
+       "onepass": a.onepass}
+with AlsContext(rs.user_ids, rs.item_ids, rs.ratings, a.k, rs.num_users, rs.num_items) as ctx:
+    ctx.set_option("cg_onepass", a.onepass)
+    ctx.set_factors(U0, V0)
+    ctx.iterate(3)
+    ctx.sync()
+    for side in ("users", "items"):
+        ctx.reset_stats()
+        ctx.set_timing(True)
+        its = []
+        for _ in range(a.reps):
+            it, _ = ctx.half_step(side, -1e300, a.m)
+            its.append(it)
+        st = ctx.stats()
+        ctx.set_timing(False)
+        ph = st["phase_ms"]["solve_" + side]
+        n_it = sum(its)
+        out[side] = {"cg_iterations": its, "ms_per_cg_iteration": round(ph / n_it, 4),
+                     "gram_ms": round(st["phase_ms"]["gram_" + side] / a.reps, 4),
+                     "kernels": {c: round(st["kernel_ms"][c] / max(1, st["kernel_launches"][c]) * 1e3, 2)
+                                 for c in st["kernel_ms"] if st["kernel_launches"][c]}}
+print(json.dumps(out), flush=True)
