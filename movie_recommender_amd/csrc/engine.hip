@@ -336,6 +336,12 @@ int Engine::build_side(Side& S, bool user, int64_t n, const int32_t* d_key,
   if (dalloc(&S.start_parts, 3 * std::max<int64_t>(1, S.n_start_pairs), stream)) return -1;
   // matvec grid: one wave per entity, fixed grid for reproducible partials
   int64_t g = (S.E + 3) / 4;
+  // MR_MV_PARTS (tuning experiments only): another fixed grid size
+  static const int64_t parts_env = [] {
+    const char* e = getenv("MR_MV_PARTS");
+    return e ? (int64_t)atoll(e) : (int64_t)0;
+  }();
+  if (parts_env > 0) g = std::min(g, parts_env);
   S.n_part_mv = (int)std::max<int64_t>(1, std::min<int64_t>(g, kMaxParts));
   MR_HIP(hipStreamSynchronize(stream));
   return 0;
@@ -364,7 +370,7 @@ int Engine::init(int dev, int k_, int64_t U_, int64_t I_, int64_t n_u,
                        hipHostMallocMapped | hipHostMallocCoherent));
   memset(h_mirror, 0, kMirrorSlots * sizeof(CgMirror));
   MR_HIP(hipHostGetDevicePointer((void**)&d_mirror, h_mirror, 0));
-  if (dalloc(&d_state, 1, stream) || dalloc(&partials, 3 * kMaxParts, stream) ||
+  if (dalloc(&d_state, 1, stream) || dalloc(&partials, 4 * kMaxParts, stream) ||
       dalloc(&d_flag, 4, stream))
     return -1;
   // every field defined before any kernel reads it: the fused CG start
@@ -501,13 +507,13 @@ int Engine::set_rccl(const unsigned char* id, int rank, int world) {
 }
 
 // Peer all-reduce of the CG scalars: this rank's exchange buffer (kPeerSlots x
-// kMaxPeers records of 4 doubles, uncached device memory so that peers'
+// kMaxPeers records of kPeerRec doubles, uncached device memory so that peers'
 // stores over xGMI are seen by this GPU's loads) and its IPC handle.
 int Engine::peer_handle(unsigned char* out64) {
   static_assert(sizeof(hipIpcMemHandle_t) == 64, "hipIpcMemHandle_t size");
   MR_HIP(hipSetDevice(device));
   if (!peer_buf) {
-    const size_t bytes = (size_t)kPeerSlots * kMaxPeers * 4 * sizeof(double);
+    const size_t bytes = (size_t)kPeerSlots * kMaxPeers * kPeerRec * sizeof(double);
     MR_HIP(hipExtMallocWithFlags((void**)&peer_buf, bytes, hipDeviceMallocUncached));
     MR_HIP(hipMemsetAsync(peer_buf, 0, bytes, stream));
     MR_HIP(hipStreamSynchronize(stream));
@@ -978,7 +984,7 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr, bool start
 
 // One-pass CG (DESIGN.md "One-pass CG iteration"): the same solve as cg()
 // with ONE kernel per CG iteration (cg_onepass_kernel: the previous
-// iteration's deferred x / r update, p, q = G p and the three sums whose last
+// iteration's deferred x / r update, p, q = G p and the four sums whose last
 // block takes alpha, r'.r' and the BETA rule, and publishes) and a finish
 // launch that applies the last iteration's update after the stop.  The
 // state after iteration t is published by kernel t (by the CG_START control

@@ -758,7 +758,13 @@ __device__ __forceinline__ void bf3_split(u32x4_t (&P)[3][NB], float (&cacc)[NB]
 //     8-pass XDL result -> VALU / v_accvgpr_read needs NumPasses + 3 (+1 on
 //     gfx950) = 12 wait states; three s_nop give 8 + 8 + 4 = 20.
 // sched_barrier(0) on both sides keeps the scheduler from moving any
-// instruction across a guard.
+// instruction across a guard.  In the built code the compiler's accumulator
+// copies (v_accvgpr_read) still land above the exit guard's nops: the wait
+// states the epilogue actually gets come from the loop tail (bf3_split of the
+// next tile, > 250 instructions after the last MFMA, no forward branch).
+// tests/test_asm_guards.py disassembles the gfx950 code object and counts
+// both gaps on every NB >= 5 instance, so a change that shortens them fails
+// the CPU suite.
 __device__ __forceinline__ void mfma_entry_guard() {
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 4");
@@ -1559,7 +1565,7 @@ __device__ __forceinline__ void apply_beta(CgScalars& v, double rr2) {
   }
 }
 
-// Peer all-reduce of `count` (<= 3) doubles by ONE thread (the finalizing
+// Peer all-reduce of `count` (< kPeerRec) doubles by ONE thread (the finalizing
 // thread of a kernel whose blocks have all finished): write this rank's
 // values into its record of every rank's exchange buffer, tag it with the
 // reduction's sequence number (release, system scope), wait for the tags of
@@ -1577,17 +1583,17 @@ __device__ bool peer_sum(PeerComm* pc, double* vals, int count) {
   const int world = pc->world, rank = pc->rank;
   const int64_t slot = s % kPeerSlots;
   for (int q = 0; q < world; ++q) {
-    double* rec = pc->buf[q] + (slot * world + rank) * 4;
+    double* rec = pc->buf[q] + (slot * world + rank) * kPeerRec;
     for (int c = 0; c < count; ++c)
       __hip_atomic_store(rec + c, vals[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(reinterpret_cast<uint64_t*>(rec + 3), (uint64_t)s, __ATOMIC_RELEASE,
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(rec + kPeerRec - 1), (uint64_t)s, __ATOMIC_RELEASE,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  double acc[3] = {0.0, 0.0, 0.0};
+  double acc[kPeerRec - 1] = {};
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
   for (int q = 0; q < world; ++q) {
-    const double* rec = pc->buf[rank] + (slot * world + q) * 4;
-    while (__hip_atomic_load(reinterpret_cast<const uint64_t*>(rec + 3), __ATOMIC_ACQUIRE,
+    const double* rec = pc->buf[rank] + (slot * world + q) * kPeerRec;
+    while (__hip_atomic_load(reinterpret_cast<const uint64_t*>(rec + kPeerRec - 1), __ATOMIC_ACQUIRE,
                              __HIP_MEMORY_SCOPE_SYSTEM) != (uint64_t)s) {
       if (__builtin_amdgcn_s_memrealtime() - t0 > 3000000000ull) {
         pc->error = 1;
@@ -1854,13 +1860,16 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 4 : 2)) void cg_matvec_kernel(
 // CG iteration t >= 1 instead of matvec + update.  Each wave first applies,
 // for its entity, iteration t-1's deferred update (x += alpha p, r += alpha q:
 // matrix.cpp:501-503, the same fp64 expressions as cg_update_kernel), then
-// p = -r + beta p (:521), q = G p, and adds p.q, r.q and q.q to its partials.
-// The last-arriving block sums them in a fixed order and takes iteration t's
-// scalars: alpha = r.r / p.q (:497) and, without a second pass over the
-// vectors, r'.r' = r.r + 2 alpha r.q + alpha^2 q.q for the new residual
-// r' = r + alpha q -- the same quantity as the reference's direct r'.r'
-// (:507) up to rounding of order eps r.r / r'.r' (CG's per-iteration decrease
-// is moderate, see the design note) -- then the BETA rule and the publish.
+// p = -r + beta p (:521), q = G p, and adds p.q, r.q, q.q and the updated
+// residual's own r.r to its partials.  The last-arriving block sums them in a
+// fixed order and takes iteration t's scalars: alpha = r.r / p.q (:497) with
+// the direct r.r and, without a second pass over the vectors, r'.r' = r.r +
+// 2 alpha r.q + alpha^2 q.q for the new residual r' = r + alpha q -- the same
+// quantity as the reference's direct r'.r' (:507) up to rounding of order
+// eps r.r / r'.r' (CG's per-iteration decrease is moderate, see the design
+// note) -- then the BETA rule and the publish.  The derived value sets only
+// that beta and stop test: kernel t+1 replaces it by the direct dot, so its
+// rounding does not accumulate over the solve.
 // Iteration t's own update is deferred to kernel t+1 or, after the stop, to
 // cg_update_kernel(UPD_FINISH).  `update` = 0 for t = 0 of an unfused start
 // (nothing deferred yet).  Per vector entry: read p, r, q, x; write p, r, q, x
@@ -1888,11 +1897,11 @@ __global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 :
   __shared__ MvScratch<NB> scr[MV_WAVES];
   __shared__ double rvs[MV_WAVES][16 * NB];
   __shared__ double sh[MV_WAVES];
-  __shared__ double wacc[MV_WAVES][3];   // the wave's running p.q, r.q, q.q (off the VGPRs)
+  __shared__ double wacc[MV_WAVES][4];   // the wave's running p.q, r.q, q.q, r.r (off the VGPRs)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   MvScratch<NB>& sc = scr[wid];
   double* rs = rvs[wid];
-  if (lane < 3) wacc[wid][lane] = 0.0;
+  if (lane < 4) wacc[wid][lane] = 0.0;
   for (int64_t e = (int64_t)blockIdx.x * MV_WAVES + wid; e < E;
        e += (int64_t)gridDim.x * MV_WAVES) {
     double* pe = p + e * ldk;
@@ -1911,6 +1920,7 @@ __global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 :
     }
     double pbias = 0.0, rbias = 0.0, qbias = 0.0;
     float xbias = 0.f;
+    double d = 0.0;   // r.r of the updated residual (matrix.cpp:507's direct dot)
     if (USER) {
       pbias = pb[e];
       rbias = rb[e];
@@ -1939,6 +1949,7 @@ __global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 :
           xe[i] = (float)fma(alpha, pi[h], (double)xi[h]);
           pn = fma(beta, pi[h], -rn);
           pe[i] = pn;
+          d = fma(rn, rn, d);
         }
         sc.pv[virt_of(i, NB)] = pn;
         rs[virt_of(i, NB)] = rn;
@@ -1954,6 +1965,7 @@ __global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 :
       }
       rbias = rbn;
       pbias = pbn;
+      if (lane == 0) d = fma(rbn, rbn, d);
     }
     if (NF > 0 && lane < 16 * NF) sc.dd[lane] = d2;
     __builtin_amdgcn_wave_barrier();
@@ -1983,19 +1995,21 @@ __global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 :
     a = wave_sum_f64(a);
     b = wave_sum_f64(b);
     c = wave_sum_f64(c);
+    d = wave_sum_f64(d);
     if (lane == 0) {
       wacc[wid][0] += a;
       wacc[wid][1] += b;
       wacc[wid][2] += c;
+      wacc[wid][3] += d;
     }
     __builtin_amdgcn_wave_barrier();
   }
   const int64_t np = gridDim.x;
-  double tot[3];
+  double tot[4];
   __syncthreads();
   if (threadIdx.x == 0) {   // waves in order, as block_sum_f64 sums them
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
+    for (int j = 0; j < 4; ++j) {
       double t = 0.0;
       for (int w = 0; w < MV_WAVES; ++w) t += wacc[w][j];
       tot[j] = t;
@@ -2003,7 +2017,7 @@ __global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 :
   }
   if (threadIdx.x == 0) {
 #pragma unroll
-    for (int j = 0; j < 3; ++j)
+    for (int j = 0; j < 4; ++j)
       __hip_atomic_store(&partials[j * np + blockIdx.x], tot[j], __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -2017,9 +2031,9 @@ __global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 :
   }
   __syncthreads();
   if (!s_last) return;
-  double sum[3];
+  double sum[4];
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
+  for (int j = 0; j < 4; ++j) {
     double acc = 0.0;
     for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x)
       acc += __hip_atomic_load(&partials[j * np + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2029,12 +2043,17 @@ __global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 :
   if (threadIdx.x == 0) {
     __hip_atomic_store(&st->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (PeerComm* pc = ald(&st->peer)) {
-      if (!peer_sum(pc, sum, 3)) {
+      if (!peer_sum(pc, sum, 4)) {
         peer_fail(st, mirror, seq);
         return;
       }
     }
     CgScalars v = load_state(st);
+    // iteration t >= 1: alpha and the next r'.r' start from the DIRECT r.r of
+    // the residual just updated, not from the previous kernel's derived value,
+    // so the derivation's rounding does not accumulate across iterations
+    // (the derived value set only the previous beta and stop test)
+    if (update) v.rr = sum[3];
     const double al = v.rr / sum[0];
     v.alpha = al;
     v.n_matvec += 1;

@@ -174,12 +174,13 @@ struct CgStart {
 
 // Peer all-reduce of the CG scalars over IPC-mapped device memory (sharded
 // runs; Engine::set_peer).  Every rank owns an exchange buffer of
-// kPeerSlots x world records {v0, v1, -, tag} in uncached device memory and
+// kPeerSlots x world records {v0 .. v6, tag} in uncached device memory and
 // maps every peer's.  Reduction s writes this rank's values into record
 // (s % kPeerSlots, rank) of EVERY rank's buffer, then the tag s (release,
 // system scope); each rank then waits for the tag of every record of its own
 // buffer and sums the values in rank order -- so all ranks get the same bits.
 constexpr int kPeerSlots = 16;
+constexpr int kPeerRec = 8;    // doubles per record: up to 7 values, then the tag
 constexpr int kMaxPeers = 64;
 struct PeerComm {
   int32_t world, rank;

@@ -1,0 +1,120 @@
+"""CPU: the gfx950 code object of the built library, disassembled, keeps the
+explicit wait states around the inline-asm MFMAs of the Gram kernel (NB >= 5,
+k > 64: kernels.hip mfma_entry_guard / mfma_exit_guard; an asm statement is
+opaque to LLVM's hazard recognizer, cdna_hip_programming.md section 5.7).
+A scheduling or compiler change that moved an accumulator read or a VALU
+write next to the MFMAs would make wrong normal equations without a fault;
+this check fails the build instead.
+
+For every gram_kernel<NB >= 5> instance:
+  * every run of consecutive v_mfma instructions (s_nop pads between them
+    allowed) is entered through an s_nop of >= 3 wait states (the guard's
+    `s_nop 4`; VALU writes of P / the zeroed accumulators -> SrcA/B/C need
+    <= 2);
+  * no v_accvgpr_read / write inside a run (the accumulators stay pinned);
+  * between the last v_mfma and the first later instruction touching the
+    accumulators (v_accvgpr_read, or an AGPR source), >= 12 wait states on
+    the straight-line fall-through path (8-pass XDL result -> reader; an
+    issued instruction counts 1, `s_nop n` counts n + 1), with no forward
+    branch that could skip them.  The compiler hoists the accumulator copies
+    above mfma_exit_guard's nops, so in the built code the wait states come
+    from the loop tail (the next tile's split/gather, hundreds of
+    instructions) ahead of the loop's back edge; the check counts whatever
+    is actually there."""
+import os
+import re
+import shutil
+import struct
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SO = os.path.join(ROOT, "movie_recommender_amd", "lib", "cpp_ls_lib.so")
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+def _gfx950_objects(so):
+    sec = subprocess.run([f"{LLVM}/llvm-readelf", "-S", so], capture_output=True,
+                         text=True).stdout
+    line = next(l for l in sec.splitlines() if ".hip_fatbin" in l)
+    f = line.split("]")[1].split()
+    off, size = int(f[3], 16), int(f[4], 16)
+    with open(so, "rb") as fh:
+        fh.seek(off)
+        data = fh.read(size)
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    objs = []
+    p = data.find(magic)
+    while p >= 0:
+        n = struct.unpack_from("<Q", data, p + 24)[0]
+        q = p + 32
+        for _ in range(n):
+            eo, es, tl = struct.unpack_from("<QQQ", data, q)
+            q += 24
+            triple = data[q:q + tl].decode()
+            q += tl
+            if "gfx950" in triple and es:
+                objs.append(data[p + eo:p + eo + es])
+        p = data.find(magic, p + 1)
+    return objs
+
+
+def _functions(asm):
+    out = {}
+    for chunk in re.split(r"\n(?=[0-9a-f]{16} <)", asm):
+        m = re.match(r"[0-9a-f]{16} <([^>]+)>:", chunk)
+        if m:
+            out[m.group(1)] = [l.split("//")[0].strip() for l in chunk.splitlines()[1:]]
+    return out
+
+
+def _nop_states(ins):
+    m = re.match(r"s_nop\s+(0x[0-9a-f]+|\d+)", ins)
+    return int(m.group(1), 0) + 1 if m else 0
+
+
+def _backward(ins):
+    # llvm-objdump prints a branch target as a signed 16-bit word offset
+    # (e.g. `s_cbranch_scc0 64781` = -755): >= 0x8000 jumps back
+    m = re.search(r"\s(\d+)$", ins)
+    return bool(m) and int(m.group(1)) >= 0x8000
+
+
+@pytest.mark.skipif(not os.path.exists(SO) or not shutil.which(f"{LLVM}/llvm-objdump"),
+                    reason="library or llvm-objdump missing")
+def test_gram_mfma_wait_state_guards(tmp_path):
+    checked = 0
+    for j, obj in enumerate(_gfx950_objects(SO)):
+        path = tmp_path / f"co{j}.o"
+        path.write_bytes(obj)
+        asm = subprocess.run([f"{LLVM}/llvm-objdump", "-d", str(path)], capture_output=True,
+                             text=True).stdout
+        for name, lines in _functions(asm).items():
+            m = re.search(r"gram_kernelILi(\d+)E", name)
+            if not m or int(m.group(1)) < 5:
+                continue
+            ins = [l.split(None, 1)[1] if re.match(r"^[0-9a-f]+:?\s", l) else l
+                   for l in lines if l and not l.endswith(":")]
+            ins = [re.sub(r"^([0-9a-f]{8}\s)+", "", i).strip() for i in ins]
+            ins = [i for i in ins if i]
+            mf = [t for t, i in enumerate(ins) if i.startswith("v_mfma")]
+            assert mf, name
+            runs = []   # consecutive MFMAs (the compiler may pad asm boundaries with s_nop)
+            for t in mf:
+                if runs and all(i.startswith("s_nop") for i in ins[runs[-1][1] + 1:t]):
+                    runs[-1][1] = t
+                else:
+                    runs.append([t, t])
+            for a, b in runs:
+                assert _nop_states(ins[a - 1]) >= 3, (name, ins[a - 3:a + 1])
+                assert not any("accvgpr" in i for i in ins[a:b + 1]), name
+            last = mf[-1]
+            nxt = next(t for t in range(last + 1, len(ins))
+                       if "accvgpr" in ins[t] or re.search(r"\ba\d+|\ba\[", ins[t]))
+            gap = ins[last + 1:nxt]
+            fwd = [i for i in gap if re.match(r"s_(c)?branch", i) and not _backward(i)]
+            assert not fwd, (name, fwd)
+            assert sum(_nop_states(i) or 1 for i in gap) >= 12, (name, gap)
+            checked += 1
+    assert checked >= 16     # NB = 5..8 x user/item x fused/unfused (x buffer forms)
