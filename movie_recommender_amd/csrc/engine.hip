@@ -335,14 +335,25 @@ int Engine::build_side(Side& S, bool user, int64_t n, const int32_t* d_key,
   S.n_start_pairs = gram_blocks(S.n_work) + (S.n_split + 3) / 4;
   if (dalloc(&S.start_parts, 3 * std::max<int64_t>(1, S.n_start_pairs), stream)) return -1;
   // matvec grid: one wave per entity, fixed grid for reproducible partials
-  int64_t g = (S.E + 3) / 4;
-  // MR_MV_PARTS (tuning experiments only): another fixed grid size
+  const int64_t g = (S.E + 3) / 4;
+  S.n_part_mv = (int)std::max<int64_t>(1, std::min<int64_t>(g, kMaxParts));
+  // one-pass CG kernel: exactly the blocks the chip holds at once (a second,
+  // partial round of blocks measured up to 30 % slower: users k = 64, 3
+  // blocks per CU, 768 blocks 216 us, 1024 blocks 286 us, 2048 blocks 238
+  // us); MR_MV_PARTS overrides it for tuning experiments
   static const int64_t parts_env = [] {
     const char* e = getenv("MR_MV_PARTS");
     return e ? (int64_t)atoll(e) : (int64_t)0;
   }();
-  if (parts_env > 0) g = std::min(g, parts_env);
-  S.n_part_mv = (int)std::max<int64_t>(1, std::min<int64_t>(g, kMaxParts));
+  int64_t op = g;
+  if (k <= kMaxK) {
+    int cus = 0;
+    MR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    const int bpc = onepass_blocks_per_cu(S.user, k);
+    if (bpc > 0 && cus > 0) op = std::min<int64_t>(op, (int64_t)bpc * cus);
+  }
+  if (parts_env > 0) op = std::min(g, parts_env);
+  S.n_part_op = (int)std::max<int64_t>(1, std::min<int64_t>(op, kMaxParts));
   MR_HIP(hipStreamSynchronize(stream));
   return 0;
 }
@@ -1048,7 +1059,7 @@ int Engine::cg_onepass(Side& S, double min_dec, int max_it, double* final_rr, bo
     hipEvent_t ev = nullptr;
     if (tic(mv_cls, t, &ev)) return -1;
     if (launch_cg_onepass(stream, user, d_state, t > 0 ? 1 : 0, S.E, k, S.G, S.Gs, S.Gn, S.p,
-                          S.pb, S.r, S.rb, S.q, S.qb, xf, xb, partials, S.n_part_mv, d_mirror,
+                          S.pb, S.r, S.rb, S.q, S.qb, xf, xb, partials, S.n_part_op, d_mirror,
                           seq_of.back()))
       return -1;
     return toc(mv_cls, t, ev);

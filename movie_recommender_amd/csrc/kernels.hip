@@ -154,7 +154,7 @@ struct MvScratch {
 // row sums and count.  The user-side bias column Gs vb is added to every y.
 // A diagonal block contributes only its stored triangle (the bf16x3 MFMA sum
 // is not bitwise symmetric; mr_internal.h).
-template <int NB, bool USER>
+template <int NB, bool USER, bool OPAQUE = (NB > 4)>
 __device__ __forceinline__ void tile_matvec(
     const float4 (&g)[NB * (NB - 1) / 2 + NB / 2 + (NB & 1)], MvScratch<NB>& sc, double vb,
     const float* __restrict__ Gs_e, float gn, int k, double (&yo)[(16 * NB + 63) / 64],
@@ -170,7 +170,7 @@ __device__ __forceinline__ void tile_matvec(
     // merge the conversions: 352 -> 256 VGPRs, 2 waves/SIMD at k = 128; the
     // values are the same, so the results are bit-identical).  At NB <= 4 the
     // merged form fits 4 waves/SIMD and measured faster.
-    if constexpr (NB > 4) asm volatile("" : "+v"(gg.x), "+v"(gg.y), "+v"(gg.z), "+v"(gg.w));
+    if constexpr (OPAQUE) asm volatile("" : "+v"(gg.x), "+v"(gg.y), "+v"(gg.z), "+v"(gg.w));
     ge[0] = gg.x; ge[1] = gg.y; ge[2] = gg.z; ge[3] = gg.w;
   };
   // diagonal tile of block b and whether its stored triangle is the lower one
@@ -758,21 +758,40 @@ __device__ __forceinline__ void bf3_split(u32x4_t (&P)[3][NB], float (&cacc)[NB]
 //     8-pass XDL result -> VALU / v_accvgpr_read needs NumPasses + 3 (+1 on
 //     gfx950) = 12 wait states; three s_nop give 8 + 8 + 4 = 20.
 // sched_barrier(0) on both sides keeps the scheduler from moving any
-// instruction across a guard.  In the built code the compiler's accumulator
-// copies (v_accvgpr_read) still land above the exit guard's nops: the wait
-// states the epilogue actually gets come from the loop tail (bf3_split of the
-// next tile, > 250 instructions after the last MFMA, no forward branch).
-// tests/test_asm_guards.py disassembles the gfx950 code object and counts
-// both gaps on every NB >= 5 instance, so a change that shortens them fails
-// the CPU suite.
+// instruction across a guard.  A plain nop statement is not enough after the
+// last MFMA: the compiler placed its accumulator copies (v_accvgpr_read)
+// right behind the MFMA, above the nops, so the exit guard takes every
+// accumulator as an operand (below).  tests/test_asm_guards.py disassembles
+// the gfx950 code object and counts both gaps on every NB >= 5 instance, so a
+// change that shortens them fails the CPU suite.
 __device__ __forceinline__ void mfma_entry_guard() {
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 4");
   __builtin_amdgcn_sched_barrier(0);
 }
-__device__ __forceinline__ void mfma_exit_guard() {
+// The exit guard names every accumulator as an in/out AGPR operand (the nop
+// statement first, then operand-only statements in groups of four, volatile
+// and so kept in order): a read of any accumulator -- including the copies
+// the compiler makes for the epilogue -- depends on a statement at or after
+// the nops and cannot be scheduled between the last MFMA and them.
+template <int T>
+__device__ __forceinline__ void mfma_exit_guard(floatx4 (&acc)[T]) {
+  static_assert(T >= 4, "NB >= 5 only");
   __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3");
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3"
+               : "+a"(acc[0]), "+a"(acc[1]), "+a"(acc[2]), "+a"(acc[3]));
+#pragma unroll
+  for (int g = 4; g < T; g += 4) {
+    __builtin_amdgcn_sched_barrier(0);
+    if (g + 3 < T)
+      asm volatile("" : "+a"(acc[g]), "+a"(acc[g + 1]), "+a"(acc[g + 2]), "+a"(acc[g + 3]));
+    else if (g + 2 < T)
+      asm volatile("" : "+a"(acc[g]), "+a"(acc[g + 1]), "+a"(acc[g + 2]));
+    else if (g + 1 < T)
+      asm volatile("" : "+a"(acc[g]), "+a"(acc[g + 1]));
+    else
+      asm volatile("" : "+a"(acc[g]));
+  }
   __builtin_amdgcn_sched_barrier(0);
 }
 
@@ -893,8 +912,11 @@ __device__ __forceinline__ void gram_wave(
   u32x4_t P[3][NB];
   gather_half<NB, BUF>(Fr, w, fin32(h0, 0), src, row_bytes);
   bf3_split<NB, USER>(P, cacc, sacc, wsum, Fr, w);
+  // the last half is peeled: its iteration would gather and split a half
+  // past the end (zero rows, weight 0) that no MFMA uses -- about one half's
+  // VALU work per work item (users: ~6 halves each)
   const int nhalves = (wlen + 31) >> 5;
-  for (int h = 0; h < nhalves; ++h) {
+  for (int h = 0; h < nhalves - 1; ++h) {
     const ChunkRaw h3 = ld32(h + 3);
     bias32(h2, h + 2);
     gather_half<NB, BUF>(Fr, w, fin32(h1, h + 1), src, row_bytes);
@@ -904,7 +926,8 @@ __device__ __forceinline__ void gram_wave(
     h1 = h2;
     h2 = h3;
   }
-  if constexpr (NB >= 5) mfma_exit_guard();
+  if (nhalves > 0) bf3_mfma<NB>(acc, P);
+  if constexpr (NB >= 5) mfma_exit_guard(acc);
 
   // ---- epilogue -----------------------------------------------------------
 #pragma unroll
@@ -1881,6 +1904,9 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 4 : 2)) void cg_matvec_kernel(
 #ifndef MR_OP_WAVES_U4
 #define MR_OP_WAVES_U4 3
 #endif
+#ifndef MR_OP_OPAQUE
+#define MR_OP_OPAQUE 0
+#endif
 template <int NB, bool USER>
 __global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 : 4) : 2)) void cg_onepass_kernel(
     CgState* __restrict__ st, int update, int64_t E, int k, int ldk,
@@ -1970,7 +1996,8 @@ __global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 :
     if (NF > 0 && lane < 16 * NF) sc.dd[lane] = d2;
     __builtin_amdgcn_wave_barrier();
     double yo[NV], ybv = 0.0;
-    tile_matvec<NB, USER>(g, sc, pbias, USER ? Gs + e * ldk : nullptr, USER ? Gn[e] : 0.f, k, yo,
+    tile_matvec<NB, USER, (NB > 4) || MR_OP_OPAQUE>(g, sc, pbias, USER ? Gs + e * ldk : nullptr,
+                                                    USER ? Gn[e] : 0.f, k, yo,
                           ybv);
     double a = 0.0, b = 0.0, c = 0.0;
 #pragma unroll
@@ -2062,6 +2089,23 @@ __global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 :
     ast(&st->pending, 1);
     publish(v, mirror, seq);
   }
+}
+
+int onepass_blocks_per_cu(bool user_side, int k) {
+  const void* f = nullptr;
+#define MR_OP_FN(NB)                                                                        \
+  case NB:                                                                                  \
+    f = user_side ? (const void*)cg_onepass_kernel<NB, true> : (const void*)cg_onepass_kernel<NB, false>; \
+    break;
+  switch (nb16_of(k)) {
+    MR_OP_FN(1) MR_OP_FN(2) MR_OP_FN(3) MR_OP_FN(4)
+    MR_OP_FN(5) MR_OP_FN(6) MR_OP_FN(7) MR_OP_FN(8)
+    default: return 0;
+  }
+#undef MR_OP_FN
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, 256, 0) != hipSuccess) return 0;
+  return n;
 }
 
 int launch_cg_onepass(hipStream_t s, bool user_side, CgState* st, int update, int64_t E, int k,

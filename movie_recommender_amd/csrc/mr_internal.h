@@ -270,6 +270,9 @@ int launch_cg_matvec(hipStream_t s, bool user_side, const CgState* st,
 // iteration's deferred x / r update (update != 0), p = -r + beta p, q = G p,
 // p.q / r.q / q.q partials (3 x n_part doubles in partials) and, in the last
 // block, alpha, r'.r', the BETA rule and the publish under `seq`.  k <= 128.
+// Blocks of cg_onepass_kernel one CU holds at once for this side and k (0:
+// unknown); the one-pass grid is that times the CU count.
+int onepass_blocks_per_cu(bool user_side, int k);
 int launch_cg_onepass(hipStream_t s, bool user_side, CgState* st, int update, int64_t E, int k,
                       const float* G, const float* Gs, const float* Gn, double* p, double* pb,
                       double* r, double* rb, double* q, double* qb, float* x, float* xb,
