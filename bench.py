@@ -252,7 +252,7 @@ def main():
     ap.add_argument("--scalars", default="peer", choices=["peer", "collective"],
                     help="sharded runs: CG scalars through the peer all-reduce (IPC-mapped "
                          "buffers; falls back to RCCL if its self-test fails) or RCCL")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r02.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r03.json"),
                     help="per-kernel HBM bytes from a rocprofv3 --pmc run (optional)")
     args = ap.parse_args()
 
@@ -404,11 +404,13 @@ def main():
     avg_s = tot_ms / launches / 1e3
     _, nU, _ = ctx.local_size("users")
     _, nI, n_local_items = ctx.local_size("items")
-    # one-pass CG: unsharded or with peer scalars (RCCL collectives: two kernels)
+    # one-pass CG: unsharded or with peer scalars (RCCL collectives: two
+    # kernels), and not on the user side at k > 64 (Engine::cg)
     onepass = (not args.no_onepass and k <= 128
                and (dist is None or getattr(ctx, "peer_scalars", False)))
+    onepass_of = lambda c: onepass and (not c.endswith("users") or k <= 64)  # noqa: E731
     nbytes, nflops = algorithmic_cost(cls, k, nU, nI, n_local_users, ldk, not args.no_fuse_start,
-                                      n_local_items, onepass)
+                                      n_local_items, onepass_of(cls))
     bound = "mfma" if cls.startswith("gram") and k >= 32 else "hbm"
     if bound == "hbm":
         achieved, peak, unit = nbytes / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
@@ -435,7 +437,7 @@ def main():
         n = st["kernel_launches"][c]
         if n:
             b, fl = algorithmic_cost(c, k, nU, nI, n_local_users, ldk, not args.no_fuse_start,
-                                     n_local_items, onepass)
+                                     n_local_items, onepass_of(c))
             kernel_table[c] = {"total_ms": round(ms, 3), "launches": n,
                                "avg_us": round(ms / n * 1e3, 2),
                                "alg_GBps": round(b / (ms / n / 1e3) / 1e9, 1) if b else None,
@@ -465,7 +467,8 @@ def main():
                                    else "single"),
                    "cg_scalars": ("peer all-reduce (IPC)" if getattr(ctx, "peer_scalars", False)
                                   else "rccl all-reduce" if dist is not None else "local"),
-                   "cg_iteration": "one pass" if onepass else "matvec + update"},
+                   "cg_iteration": ("matvec + update" if not onepass else "one pass"
+                                    if k <= 64 else "one pass (items), matvec + update (users)")},
         "roofline": {"kernel": cls, "bound": bound, "achieved": round(achieved, 2),
                      "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
                      "traffic": traffic,

@@ -831,7 +831,12 @@ int Engine::x_ptrs(Side& S, float** xf, float** xb) {
 // that t cannot terminate (fails == 0, rr far above 1e-6, t+1 < max_it) --
 // so the stream stays busy without launching iterations that would be idle.
 int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr, bool started) {
-  if (onepass && k <= kMaxK && (!sharded() || peer_on))
+  // one pass per CG iteration everywhere except the user side at k > 64:
+  // there the one-pass kernel (32 tiles + the deferred-update vectors at 2
+  // waves / SIMD) spills 18 registers and measured 3 % slower per CG
+  // iteration than matvec + update (k = 128, ML-full, fixed 20 iterations:
+  // 0.286 vs 0.278 ms); the item side gains 13 % there
+  if (onepass && k <= kMaxK && (!S.user || nb16_of(k) <= 4) && (!sharded() || peer_on))
     return cg_onepass(S, min_dec, max_it, final_rr, started);
   float *xf, *xb;
   x_ptrs(S, &xf, &xb);

@@ -1898,14 +1898,16 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 4 : 2)) void cg_matvec_kernel(
 // (nothing deferred yet).  Per vector entry: read p, r, q, x; write p, r, q, x
 // (56 B fp64/fp32) against 72 B for matvec + update, and one kernel boundary
 // less per iteration.
-// Occupancy: 4 waves / SIMD (128 VGPRs) at NB <= 4 like cg_matvec_kernel,
-// except the user side at NB = 4, whose bias column needs a few registers
-// more than 128 (14 spilled registers at 4 waves): 3 waves / SIMD.
+// Occupancy: 4 waves / SIMD (<= 128 VGPRs) at NB <= 4.  The tiles' fp64
+// copies are made afresh in each of tile_matvec's two passes (OPAQUE, as at
+// NB > 4): with the merged copies the user side at NB = 4 needed 140 VGPRs
+// (3 waves / SIMD, or 14 spilled registers at 4); now 110.  Same box, fixed
+// 20 CG iterations, k = 64: users 215 -> 211 us per iteration.
 #ifndef MR_OP_WAVES_U4
-#define MR_OP_WAVES_U4 3
+#define MR_OP_WAVES_U4 4
 #endif
 #ifndef MR_OP_OPAQUE
-#define MR_OP_OPAQUE 0
+#define MR_OP_OPAQUE 1
 #endif
 template <int NB, bool USER>
 __global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 : 4) : 2)) void cg_onepass_kernel(

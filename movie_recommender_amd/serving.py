@@ -60,6 +60,9 @@ class MovieTable:
         self.cand_als = np.array([c[1] for c in cand], np.int32)
         self.cand_med = np.array([c[2] for c in cand], np.float64)
         self.cand_index = {int(m): c for c, m in enumerate(self.cand_mid)}
+        # movie id -> candidate index (-1: not a candidate), for array inputs
+        self._cand_lut = np.full(int(self.cand_mid.max()) + 1 if len(cand) else 1, -1, np.int32)
+        self._cand_lut[self.cand_mid] = np.arange(len(cand), dtype=np.int32)
         L = _lib.lib()
         self._h = L.mr_rec_create(int(device), self.k, self.n_als, _dp(V), len(cand),
                                   _ip(self.cand_als), _ip(self.cand_mid), _dp(self.cand_med))
@@ -155,11 +158,16 @@ class MovieTable:
 
     def top_n_arrays(self, X, rated=None, num_results=ROTATION_SIZE * 100):
         """``top_n`` as arrays: movie ids int32[B, n], scores f64[B, n] and
-        the count per user (row u is valid up to count[u])."""
+        the count per user (row u is valid up to count[u]).  ``rated`` is a
+        sequence of per-user movie-id containers, or -- without any Python
+        loop over users -- a CSR pair ``(offsets int64[B + 1], movie_ids)``."""
         X = np.ascontiguousarray(np.atleast_2d(X), np.float64)
         B, N = X.shape[0], int(num_results)
         excl_off = excl = None
-        if rated is not None:
+        if isinstance(rated, tuple) and len(rated) == 2 and isinstance(rated[0], np.ndarray):
+            excl_off, excl = self._exclusions_csr(np.asarray(rated[0], np.int64),
+                                                  np.asarray(rated[1], np.int64), B)
+        elif rated is not None:
             lists = [[self.cand_index[m] for m in r if m in self.cand_index] for r in rated]
             excl_off = np.zeros(B + 1, np.int64)
             excl_off[1:] = np.cumsum([len(l) for l in lists])
@@ -173,6 +181,21 @@ class MovieTable:
             _ip(excl) if excl is not None else None, N, _ip(mids), _dp(sc), _ip(cnt)),
             "mr_rec_top_n")
         return mids, sc, cnt
+
+    def _exclusions_csr(self, off, mids, B):
+        """Rated-movie lists given as CSR (offsets, movie ids) -> candidate
+        indices per user, dropping ids that are not candidates (as the
+        container path does), vectorised."""
+        if off.shape != (B + 1,) or off[0] != 0 or np.any(np.diff(off) < 0) or off[-1] != len(mids):
+            raise ValueError("rated offsets must be int64[B + 1], non-decreasing, from 0 to len(ids)")
+        ok = (mids >= 0) & (mids < len(self._cand_lut))
+        c = np.full(len(mids), -1, np.int32)
+        c[ok] = self._cand_lut[mids[ok]]
+        keep = c >= 0
+        kept = np.concatenate([[0], np.cumsum(keep, dtype=np.int64)])
+        excl_off = np.ascontiguousarray(kept[off], np.int64)
+        excl = np.ascontiguousarray(c[keep] if keep.any() else np.zeros(1, np.int32), np.int32)
+        return excl_off, excl
 
     # -- evaluation -----------------------------------------------------------
     def evaluate(self, U, user_rows, test_lists):

@@ -90,6 +90,14 @@ def test_top_n_large_synthetic(gpu):
         cand = np.array(t.cand_mid)
         for u in range(300):
             assert got[u] == exact_top_n(S[u], cand, rated[u], 400), u
+        # the same exclusions as a CSR pair of arrays (no per-user Python
+        # loop), with non-candidate ids mixed in: identical arrays
+        lists = [np.array(sorted(r) + [10 ** 7 + u], np.int64) for u, r in enumerate(rated)]
+        off = np.concatenate([[0], np.cumsum([len(l) for l in lists])]).astype(np.int64)
+        m1, s1, c1 = t.top_n_arrays(X, rated, 400)
+        m2, s2, c2 = t.top_n_arrays(X, (off, np.concatenate(lists)), 400)
+        assert np.array_equal(c1, c2) and np.array_equal(m1, m2)
+        assert np.array_equal(s1.view(np.int64), s2.view(np.int64))
 
 
 @pytest.mark.parametrize("k", KS)

@@ -66,3 +66,27 @@ def test_fixture_covers_edge_cases():
     assert d["valid"][1] == 1
     # None agreements: single rating, all-equal ratings
     assert np.isnan(d["agreement"][0]) and np.isnan(d["agreement"][2])
+
+
+def test_exclusion_csr_matches_container_path():
+    """CPU: MovieTable's CSR exclusion input gives the candidate-index lists
+    the per-user container path builds (non-candidates dropped, order kept)."""
+    import numpy as np
+    from movie_recommender_amd.serving import MovieTable
+    t = MovieTable.__new__(MovieTable)
+    rs = np.random.RandomState(3)
+    t.cand_mid = np.sort(rs.choice(5000, 800, replace=False)).astype(np.int32)
+    t.cand_index = {int(m): c for c, m in enumerate(t.cand_mid)}
+    t._cand_lut = np.full(int(t.cand_mid.max()) + 1, -1, np.int32)
+    t._cand_lut[t.cand_mid] = np.arange(len(t.cand_mid), dtype=np.int32)
+    lists = [rs.choice(6000, rs.randint(0, 40), replace=False) for _ in range(50)] + [[]]
+    off = np.concatenate([[0], np.cumsum([len(l) for l in lists])]).astype(np.int64)
+    ids = np.concatenate([np.asarray(l, np.int64) for l in lists] + [np.array([-5], np.int64)])
+    off[-1] += 1          # a negative id in the last (otherwise empty) list: dropped
+    eo, ex = t._exclusions_csr(off, ids, len(lists))
+    for u, l in enumerate(lists):
+        want = [t.cand_index[int(m)] for m in l if int(m) in t.cand_index]
+        assert ex[eo[u]:eo[u + 1]].tolist() == want
+    import pytest
+    with pytest.raises(ValueError):
+        t._exclusions_csr(off[:-1], ids, len(lists))

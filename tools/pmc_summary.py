@@ -1,7 +1,7 @@
 """Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs into per-kernel HBM
 bytes per launch (profiles/pmc_<round>.json, read by bench.py).
 
-    python tools/pmc_summary.py --fetch DIR_FETCH --write DIR_WRITE --out profiles/pmc_r02.json
+    python tools/pmc_summary.py --fetch DIR_FETCH --write DIR_WRITE --out profiles/pmc_r03.json
 
 gfx950 corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE (KB) reports
 half the bytes of wide (16 B/lane) coalesced streaming reads -> x2; WRITE_SIZE
@@ -18,8 +18,8 @@ import re
 CLASSES = [
     ("gram_users", r"gram_kernel<\d+, true"),
     ("gram_items", r"gram_kernel<\d+, false"),
-    ("matvec_users", r"cg_matvec_kernel<\d+, true"),
-    ("matvec_items", r"cg_matvec_kernel<\d+, false"),
+    ("matvec_users", r"(cg_matvec_kernel|cg_onepass_kernel)<\d+, true"),
+    ("matvec_items", r"(cg_matvec_kernel|cg_onepass_kernel)<\d+, false"),
     ("slab_reduce", r"slab_reduce_kernel"),
     ("cg_update", r"cg_update_kernel"),
     ("cg_control", r"cg_control_kernel"),
