@@ -323,8 +323,9 @@ def g8():
 
 def g9():
     """G4 at the headline shape, round 3: the band of ``g8`` regenerated from
-    5 initial-factor seeds x thread counts {1, 2, 4, 8} (20 reference runs;
-    SURVEY.md 8(c) asks for >= 15), each run with its held-out RMSE, train
+    5 initial-factor seeds x thread counts {1, 2, 3, 4, 6, 8} (30 reference
+    runs; SURVEY.md 8(c) asks for >= 15 -- six runs per seed sample the
+    reference's within-seed, run-to-run chaos), each run with its held-out RMSE, train
     RMSE, ``ret`` and the reference's own quality metric, the mean per-user
     ranking agreement on the held-out 20 % (``worker_process.py:262-306`` +
     ``my_util.py:101-145``, restated in ``als_oracle.rank_agreement_mean``).
@@ -340,7 +341,7 @@ def g9():
     done = {(r["seed"], r["tc"]) for r in runs}
     for seed in range(5):
         U0, V0 = ref.init_factors(rs_.num_users, rs_.num_items, k, seed)
-        for tc in (8, 4, 2, 1):
+        for tc in (8, 4, 2, 1, 6, 3):
             if (seed, tc) in done:
                 continue
             ref.set_thread_count(tc)

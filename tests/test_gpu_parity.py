@@ -441,16 +441,17 @@ def _gpu_rank_agreement(rs, U, V, k):
 def test_band_headline_shape_heldout_rmse(gpu):
     """G4 at the headline shape (round 3): MovieLens-full-shaped synthetic
     data, k = 64, 20 % of each user's ratings held out, the reference's loop
-    with max_iteration 4, initial factors from seeds 0..4 -- against 20 runs
-    of the compiled reference (the same 5 seeds x thread counts 1, 2, 4, 8;
-    band_mlfull_k64.json from tests/golden/make_golden.py g9).  The
+    with max_iteration 4, initial factors from seeds 0..4 -- against the
+    compiled reference's runs of the same 5 seeds at several thread counts
+    (band_mlfull_k64.json from tests/golden/make_golden.py g9).  The
     reference is chaotic here (one seed's held-out RMSE moves 0.954 .. 1.007
     between its own thread counts), so the GPU is one more "thread count" of
     each seed: per seed, its held-out RMSE and its mean ranking agreement (the
     reference's own quality metric, my_util.py:101-145, computed on the GPU)
-    must lie within that seed's reference range widened by 25 % of the
-    pooled range, and the 5-seed means within the pooled range.  The GPU
-    values are reported in a warning (kept in the pytest summary)."""
+    must lie within that seed's reference range widened by W, the largest
+    range the reference itself shows between thread counts at any one seed
+    (its run-to-run chaos), and the 5-seed means within the pooled range.  The
+    GPU values are reported in a warning (kept in the pytest summary)."""
     import warnings
     from movie_recommender_amd import synth
     from movie_recommender_amd.engine import AlsContext
@@ -465,9 +466,13 @@ def test_band_headline_shape_heldout_rmse(gpu):
     assert len(band["runs"]) >= 15
     pool = {m: (min(r[m] for r in band["runs"]), max(r[m] for r in band["runs"]))
             for m in ("test_rmse", "rank_agreement")}
+    seeds = sorted({r["seed"] for r in band["runs"]})
+    chaos = {m: max(max(r[m] for r in band["runs"] if r["seed"] == sd)
+                    - min(r[m] for r in band["runs"] if r["seed"] == sd) for sd in seeds)
+             for m in pool}
     got = {"test_rmse": [], "rank_agreement": [], "train_rmse": [], "ret": []}
     report = []
-    for seed in sorted({r["seed"] for r in band["runs"]}):
+    for seed in seeds:
         U0, V0 = init_factors(rs.num_users, rs.num_items, k, seed)
         with AlsContext(rs.user_ids, rs.item_ids, rs.ratings, k, rs.num_users,
                         rs.num_items) as ctx:
@@ -489,9 +494,11 @@ def test_band_headline_shape_heldout_rmse(gpu):
         report.append(line)
         for m in ("test_rmse", "rank_agreement"):
             lo, hi = min(r[m] for r in runs), max(r[m] for r in runs)
-            w = 0.25 * (pool[m][1] - pool[m][0])
-            assert lo - w <= vals[m] <= hi + w, (seed, m, vals[m], lo, hi)
-    warnings.warn("headline-shape band (k=64, 4 ALS iterations): " + "; ".join(report))
+            assert lo - chaos[m] <= vals[m] <= hi + chaos[m], (seed, m, vals[m], lo, hi, chaos[m])
+    warnings.warn("headline-shape band (k=64, 4 ALS iterations, %d reference runs; within-seed "
+                  "chaos W: RMSE %.5f, agreement %.5f): " % (len(band["runs"]), chaos["test_rmse"],
+                                                              chaos["rank_agreement"])
+                  + "; ".join(report))
     for m in ("test_rmse", "rank_agreement"):
         assert pool[m][0] <= np.mean(got[m]) <= pool[m][1], (m, got[m], pool[m])
 
