@@ -516,6 +516,213 @@ __global__ __launch_bounds__(256) void k_score_t(int n_users, int n_cand, int k,
   }
 }
 
+template <bool STORE, int DIAG>
+__global__ __launch_bounds__(256) void k_score_x(int n_users, int n_cand, int k, const double* __restrict__ X,
+                                                 const double* __restrict__ Vc, const double* __restrict__ med,
+                                                 uint64_t* __restrict__ out, unsigned long long* kmin,
+                                                 unsigned long long* kmax) {
+  __shared__ __attribute__((aligned(16))) double xs[SC_KC][T_XP];
+  __shared__ double vs[SC_KC][T_VP];
+  const int tid = threadIdx.x, tx = tid & 63, ty = tid >> 6;
+  const int c0 = blockIdx.x * SC_C, u0 = blockIdx.y * SC_U;
+  double acc[8][4];
+#pragma unroll
+  for (int p = 0; p < 8; ++p)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[p][q] = 0.0;
+  const int jj = tid & 15, rr = tid >> 4;
+  double vreg[SC_C / 16], xreg[2];
+  auto load_chunk = [&](int j0) {
+    const int kc = min(SC_KC, k - j0);
+    const bool jok = jj < kc;
+    const double* src = Vc + (int64_t)(c0 + rr) * k + j0 + jj;
+#pragma unroll
+    for (int i = 0; i < SC_C / 16; ++i) {
+      const bool ok = jok && (c0 + rr + 16 * i) < n_cand;
+      vreg[i] = ok ? src[(int64_t)16 * i * k] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = rr + 16 * i, u = u0 + r;
+      xreg[i] = (jok && u < n_users) ? X[(int64_t)u * (k + 1) + j0 + jj] : 0.0;
+    }
+  };
+  load_chunk(0);
+  for (int j0 = 0; j0 < k; j0 += SC_KC) {
+    const int kc = min(SC_KC, k - j0);
+    if (DIAG != 1 || j0 == 0) {
+#pragma unroll
+    for (int i = 0; i < SC_C / 16; ++i) vs[jj][rr + 16 * i] = vreg[i];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) xs[jj][rr + 16 * i] = xreg[i];
+    }
+    __syncthreads();
+    if (DIAG != 1 && j0 + SC_KC < k) load_chunk(j0 + SC_KC);
+    double xv0[8], vv0[4];
+    if (DIAG == 2) {
+      const double2* xp = reinterpret_cast<const double2*>(&xs[0][ty * 8]);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) { const double2 t = xp[p]; xv0[2 * p] = t.x; xv0[2 * p + 1] = t.y; }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) vv0[q] = vs[0][tx + 64 * q];
+    }
+    for (int j = 0; j < kc; ++j) {
+      double xv[8], vv[4];
+      if (DIAG == 2) {
+#pragma unroll
+        for (int p = 0; p < 8; ++p) xv[p] = xv0[p] + (double)j;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) vv[q] = vv0[q];
+      } else {
+      const double2* xp = reinterpret_cast<const double2*>(&xs[j][ty * 8]);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const double2 t = xp[p];
+        xv[2 * p] = t.x;
+        xv[2 * p + 1] = t.y;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) vv[q] = vs[j][tx + 64 * q];
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        double pr[4][4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) pr[p][q] = mul_rn(xv[4 * h + p], vv[q]);
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[4 * h + p][q] = add_rn(acc[4 * h + p][q], pr[p][q]);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int u = u0 + ty * 8 + p;
+    if (u >= n_users) continue;
+    const double bias = X[(int64_t)u * (k + 1) + k];
+    unsigned long long lo = ~0ull, hi = 0ull;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = c0 + tx + 64 * q;
+      if (c >= n_cand) continue;
+      const double s = add_rn(add_rn(acc[p][q], bias), med[c]);
+      const uint64_t key = score_key(s);
+      if (STORE || key == 0x123456789ull) out[(int64_t)u * n_cand + c] = key;
+      lo = min(lo, (unsigned long long)key);
+      hi = max(hi, (unsigned long long)key);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      lo = min(lo, (unsigned long long)__shfl_xor(lo, o, 64));
+      hi = max(hi, (unsigned long long)__shfl_xor(hi, o, 64));
+    }
+    if (tx == 0) {
+      atomicMin(&kmin[u], lo);
+      atomicMax(&kmax[u], hi);
+    }
+  }
+}
+
+template <bool STORE>
+__global__ __launch_bounds__(256) void k_score_g(int n_users, int n_cand, int k, const double* __restrict__ X,
+                                                 const double* __restrict__ Vc, const double* __restrict__ med,
+                                                 uint64_t* __restrict__ out, unsigned long long* kmin,
+                                                 unsigned long long* kmax) {
+  __shared__ __attribute__((aligned(16))) double xs[SC_KC][T_XP];
+  __shared__ double vs[SC_KC][T_VP];
+  const int tid = threadIdx.x, tx = tid & 63, ty = tid >> 6;
+  // user tile fastest: the blocks in flight share a few candidate tiles
+  // (one 128 KB V tile per XCD L2) instead of streaming all of V
+  const int c0 = blockIdx.y * SC_C, u0 = blockIdx.x * SC_U;
+  double acc[8][4];
+#pragma unroll
+  for (int p = 0; p < 8; ++p)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[p][q] = 0.0;
+  const int jj = tid & 15, rr = tid >> 4;
+  double vreg[SC_C / 16], xreg[2];
+  auto load_chunk = [&](int j0) {
+    const int kc = min(SC_KC, k - j0);
+    const bool jok = jj < kc;
+    const double* src = Vc + (int64_t)(c0 + rr) * k + j0 + jj;
+#pragma unroll
+    for (int i = 0; i < SC_C / 16; ++i) {
+      const bool ok = jok && (c0 + rr + 16 * i) < n_cand;
+      vreg[i] = ok ? src[(int64_t)16 * i * k] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = rr + 16 * i, u = u0 + r;
+      xreg[i] = (jok && u < n_users) ? X[(int64_t)u * (k + 1) + j0 + jj] : 0.0;
+    }
+  };
+  load_chunk(0);
+  for (int j0 = 0; j0 < k; j0 += SC_KC) {
+    const int kc = min(SC_KC, k - j0);
+#pragma unroll
+    for (int i = 0; i < SC_C / 16; ++i) vs[jj][rr + 16 * i] = vreg[i];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) xs[jj][rr + 16 * i] = xreg[i];
+    __syncthreads();
+    if (j0 + SC_KC < k) load_chunk(j0 + SC_KC);
+    for (int j = 0; j < kc; ++j) {
+      double xv[8], vv[4];
+      const double2* xp = reinterpret_cast<const double2*>(&xs[j][ty * 8]);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const double2 t = xp[p];
+        xv[2 * p] = t.x;
+        xv[2 * p + 1] = t.y;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) vv[q] = vs[j][tx + 64 * q];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        double pr[4][4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) pr[p][q] = mul_rn(xv[4 * h + p], vv[q]);
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[4 * h + p][q] = add_rn(acc[4 * h + p][q], pr[p][q]);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int u = u0 + ty * 8 + p;
+    if (u >= n_users) continue;
+    const double bias = X[(int64_t)u * (k + 1) + k];
+    unsigned long long lo = ~0ull, hi = 0ull;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = c0 + tx + 64 * q;
+      if (c >= n_cand) continue;
+      const double s = add_rn(add_rn(acc[p][q], bias), med[c]);
+      const uint64_t key = score_key(s);
+      if (STORE || key == 0x123456789ull) out[(int64_t)u * n_cand + c] = key;
+      lo = min(lo, (unsigned long long)key);
+      hi = max(hi, (unsigned long long)key);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      lo = min(lo, (unsigned long long)__shfl_xor(lo, o, 64));
+      hi = max(hi, (unsigned long long)__shfl_xor(hi, o, 64));
+    }
+    if (tx == 0) {
+      atomicMin(&kmin[u], lo);
+      atomicMax(&kmax[u], hi);
+    }
+  }
+}
+
 template <bool STORE>
 __global__ __launch_bounds__(256) void k_score_e(int n_users, int n_cand, int k, const double* __restrict__ X,
                                                  const double* __restrict__ Vc, const double* __restrict__ med,
@@ -622,10 +829,116 @@ __global__ __launch_bounds__(256) void k_score_e(int n_users, int n_cand, int k,
   }
 }
 
+// P16 / P17: transposed LDS tiles, double-buffered in chunks of 8 factors:
+// the chunk c+1 (prefetched into registers during c-1) is written into the
+// other buffer before chunk c is multiplied, so one barrier per chunk.
+constexpr int DB_KC = 8;
+template <bool STORE>
+__global__ __launch_bounds__(256) void k_score_db(int n_users, int n_cand, int k, const double* __restrict__ X,
+                                                  const double* __restrict__ Vc, const double* __restrict__ med,
+                                                  uint64_t* __restrict__ out, unsigned long long* kmin,
+                                                  unsigned long long* kmax) {
+  __shared__ __attribute__((aligned(16))) double xs[2][DB_KC][T_XP];
+  __shared__ double vs[2][DB_KC][T_VP];
+  const int tid = threadIdx.x, tx = tid & 63, ty = tid >> 6;
+  const int c0 = blockIdx.x * SC_C, u0 = blockIdx.y * SC_U;
+  double acc[8][4];
+#pragma unroll
+  for (int p = 0; p < 8; ++p)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[p][q] = 0.0;
+  // staging map: 8 factors x 256 candidates = 2048 doubles, 8 per thread:
+  // thread (jj = tid & 7, rr = tid >> 3) loads candidates rr + 32 i
+  const int jj = tid & 7, rr = tid >> 3;
+  double vreg[SC_C / 32], xreg;
+  auto load_chunk = [&](int j0) {
+    const bool jok = j0 + jj < k;
+    const double* src = Vc + (int64_t)(c0 + rr) * k + j0 + jj;
+#pragma unroll
+    for (int i = 0; i < SC_C / 32; ++i) {
+      const bool ok = jok && (c0 + rr + 32 * i) < n_cand;
+      vreg[i] = ok ? src[(int64_t)32 * i * k] : 0.0;
+    }
+    const int u = u0 + rr;   // rr < 32: one user per thread
+    xreg = (jok && u < n_users) ? X[(int64_t)u * (k + 1) + j0 + jj] : 0.0;
+  };
+  auto store_chunk = [&](int b) {
+#pragma unroll
+    for (int i = 0; i < SC_C / 32; ++i) vs[b][jj][rr + 32 * i] = vreg[i];
+    xs[b][jj][rr] = xreg;
+  };
+  load_chunk(0);
+  store_chunk(0);
+  if (DB_KC < k) load_chunk(DB_KC);
+  __syncthreads();
+  int b = 0;
+  for (int j0 = 0; j0 < k; j0 += DB_KC) {
+    const int kc = min(DB_KC, k - j0);
+    if (j0 + DB_KC < k) {
+      store_chunk(b ^ 1);                       // chunk j0 + 8 into the other buffer
+      if (j0 + 2 * DB_KC < k) load_chunk(j0 + 2 * DB_KC);
+    }
+    for (int j = 0; j < kc; ++j) {
+      double xv[8], vv[4];
+      const double2* xp = reinterpret_cast<const double2*>(&xs[b][j][ty * 8]);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const double2 t = xp[p];
+        xv[2 * p] = t.x;
+        xv[2 * p + 1] = t.y;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) vv[q] = vs[b][j][tx + 64 * q];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        double pr[4][4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) pr[p][q] = mul_rn(xv[4 * h + p], vv[q]);
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[4 * h + p][q] = add_rn(acc[4 * h + p][q], pr[p][q]);
+      }
+    }
+    __syncthreads();
+    b ^= 1;
+  }
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int u = u0 + ty * 8 + p;
+    if (u >= n_users) continue;
+    const double bias = X[(int64_t)u * (k + 1) + k];
+    unsigned long long lo = ~0ull, hi = 0ull;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = c0 + tx + 64 * q;
+      if (c >= n_cand) continue;
+      const double s = add_rn(add_rn(acc[p][q], bias), med[c]);
+      const uint64_t key = score_key(s);
+      if (STORE || key == 0x123456789ull) out[(int64_t)u * n_cand + c] = key;
+      lo = min(lo, (unsigned long long)key);
+      hi = max(hi, (unsigned long long)key);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      lo = min(lo, (unsigned long long)__shfl_xor(lo, o, 64));
+      hi = max(hi, (unsigned long long)__shfl_xor(hi, o, 64));
+    }
+    if (tx == 0) {
+      atomicMin(&kmin[u], lo);
+      atomicMax(&kmax[u], hi);
+    }
+  }
+}
+
 // Pure fp64 VALU throughput: 32 independent chains per lane of a separate
 // multiply and add (what the exact score order needs), and the same with FMA.
 template <bool FMA>
 __global__ __launch_bounds__(256) void k_alu(double* out, double a, double b, int iters) {
+  extern __shared__ double occ_lds[];   // dynamic size only limits blocks per CU
+  if (iters < 0) occ_lds[threadIdx.x] = a;
   double acc[32];
 #pragma unroll
   for (int i = 0; i < 32; ++i) acc[i] = threadIdx.x * 1e-3 + i;
@@ -665,9 +978,11 @@ int main() {
   const char* names[] = {"P0 product", "P1 no store", "P2 lds-pipe", "P3 pipe nostore", "P4 sgpr users",
                          "P5 sgpr nostore", "P6 dpp users", "P7 dpp nostore", "P8 8x8 tile", "P9 8x8 nostore",
                          "P10 lds [j][.]", "P11 [j][.] nostore",
-                         "P12 + epilogue", "P13 + epi nostore"};
+                         "P12 + epilogue", "P13 + epi nostore", "P14 no restage", "P15 no lds in j",
+                         "P16 dbuf kc8", "P17 dbuf nostore", "P18 user-fast grid", "P19 ufast nostore"};
+  dim3 gridu(U / SC_U, (C + SC_C - 1) / SC_C);
   dim3 gridw((C + W_C - 1) / W_C, U / SC_U);
-  for (int mode = 0; mode < 14; ++mode) {
+  for (int mode = 0; mode < 20; ++mode) {
     for (int rep = 0; rep < 3; ++rep) {
       hipEventRecord(a);
       if (mode == 0) k_score<true, false><<<grid, 256>>>(U, C, k, X, V, M, O, lo, hi);
@@ -684,6 +999,12 @@ int main() {
       if (mode == 11) k_score_t<false><<<grid, 256>>>(U, C, k, X, V, M, O, lo, hi);
       if (mode == 12) k_score_e<true><<<grid, 256>>>(U, C, k, X, V, M, O, lo, hi);
       if (mode == 13) k_score_e<false><<<grid, 256>>>(U, C, k, X, V, M, O, lo, hi);
+      if (mode == 14) k_score_x<false, 1><<<grid, 256>>>(U, C, k, X, V, M, O, lo, hi);
+      if (mode == 15) k_score_x<false, 2><<<grid, 256>>>(U, C, k, X, V, M, O, lo, hi);
+      if (mode == 16) k_score_db<true><<<grid, 256>>>(U, C, k, X, V, M, O, lo, hi);
+      if (mode == 17) k_score_db<false><<<grid, 256>>>(U, C, k, X, V, M, O, lo, hi);
+      if (mode == 18) k_score_g<true><<<gridu, 256>>>(U, C, k, X, V, M, O, lo, hi);
+      if (mode == 19) k_score_g<false><<<gridu, 256>>>(U, C, k, X, V, M, O, lo, hi);
       hipEventRecord(b); hipEventSynchronize(b);
       float ms; hipEventElapsedTime(&ms, a, b);
       if (rep == 2) {
@@ -697,7 +1018,7 @@ int main() {
     uint64_t *O2;
     hipMalloc(&O2, (size_t)U * C * 8);
     k_score<true, false><<<grid, 256>>>(U, C, k, X, V, M, O, lo, hi);
-    k_score_e<true><<<grid, 256>>>(U, C, k, X, V, M, O2, lo, hi);
+    k_score_g<true><<<dim3(U / SC_U, (C + SC_C - 1) / SC_C), 256>>>(U, C, k, X, V, M, O2, lo, hi);
     hipDeviceSynchronize();
     std::vector<uint64_t> a1((size_t)C * 64), a2((size_t)C * 64);
     size_t bad = 0;
@@ -706,8 +1027,22 @@ int main() {
       hipMemcpy(a2.data(), O2 + (size_t)u0 * C, a2.size() * 8, hipMemcpyDeviceToHost);
       for (size_t i = 0; i < a1.size(); ++i) bad += a1[i] != a2[i];
     }
-    printf("P12 vs P0 keys: %zu mismatches in %zu sampled\n", bad, (size_t)8 * a1.size());
+    printf("P18 vs P0 keys: %zu mismatches in %zu sampled\n", bad, (size_t)8 * a1.size());
     hipFree(O2);
+  }
+  hipFuncSetAttribute((const void*)k_alu<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+  for (int bpc : {1, 2, 3, 4, 8}) {   // blocks (of 4 waves) per CU -> waves per SIMD
+    const size_t lds = bpc == 8 ? 0 : (size_t)(150 * 1024) / bpc;
+    const int iters = 2048, blocks = 256 * bpc * 4;
+    for (int rep = 0; rep < 3; ++rep) {
+      hipEventRecord(a);
+      k_alu<false><<<blocks, 256, lds>>>(M, 1.0000001, 1e-9, iters);
+      hipEventRecord(b); hipEventSynchronize(b);
+      float ms; hipEventElapsedTime(&ms, a, b);
+      if (rep == 2)
+        printf("ALU mul+add, %d wave(s)/SIMD: %6.2f T lane-ops/s\n", bpc,
+               (double)blocks * 256 * iters * 64 / ms / 1e9);
+    }
   }
   for (int f = 0; f < 2; ++f) {
     const int iters = 4096, blocks = 256 * 8;
