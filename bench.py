@@ -81,7 +81,8 @@ def algorithmic_cost(cls, k, n_users, n_items, n_ratings, ldk, fused=True, n_rat
     one-pass CG iteration (default) makes the matvec launch also apply the
     previous iteration's x / r update: per vector entry it reads p, r, q, x
     and writes p, r, q, x (6 x 8 + 2 x 4 B) instead of p rw, r read, q write
-    (4 x 8 B); cg_update then only runs the finish pass once per solve."""
+    (4 x 8 B); cg_update then only runs the finish pass once per solve (x +=
+    alpha p: x rw fp32, p read)."""
     K = k + 1
     nb = (k + 15) // 16
     gsz = (nb * (nb - 1) // 2 + nb // 2 + nb % 2) * 256 + (nb // 2) * 16
@@ -107,8 +108,10 @@ def algorithmic_cost(cls, k, n_users, n_items, n_ratings, ldk, fused=True, n_rat
             b += n_items * ldk * (4 + 3 * 8)
         return b, n_ri * (1.0 * k * (k + 1) + 2.0 * k)
     if cls == "cg_update":
-        # x rw (fp32), r rw, p read, q read (fp64)
         E = (n_users * (ldk + 1) + n_items * ldk) / 2.0   # average side
+        if onepass:   # the one-pass finish: x rw (fp32), p read (fp64)
+            return E * (2 * 4 + 8), E * 2.0
+        # x rw (fp32), r rw, p read, q read (fp64)
         return E * (2 * 4 + 4 * 8), E * 4.0
     return 0, 0
 
@@ -408,7 +411,7 @@ def main():
     # kernels), and not on the user side at k > 64 (Engine::cg)
     onepass = (not args.no_onepass and k <= 128
                and (dist is None or getattr(ctx, "peer_scalars", False)))
-    onepass_of = lambda c: onepass and (not c.endswith("users") or k <= 64)  # noqa: E731
+    onepass_of = lambda c: onepass and (c.endswith("items") or k <= 64)  # noqa: E731
     nbytes, nflops = algorithmic_cost(cls, k, nU, nI, n_local_users, ldk, not args.no_fuse_start,
                                       n_local_items, onepass_of(cls))
     bound = "mfma" if cls.startswith("gram") and k >= 32 else "hbm"

@@ -163,9 +163,15 @@ int mr_als_set_timing(mr_als* ctx, int enable);
  *   MR_OPT_CG_ONEPASS     1 (default): one kernel per CG iteration (the
  *                         previous iteration's x / r update deferred into
  *                         the next matvec, r'.r' from r.r, r.q, q.q; k <= 128,
- *                         unsharded or peer scalars); 0: matvec + update */
+ *                         unsharded or peer scalars, not the user side at
+ *                         k > 64); 0: matvec + update
+ *   MR_OPT_GRAM_RHS_MFMA  1 (default): the user-side Gram (32 <= k <= 128)
+ *                         takes its rhs on the matrix cores when every user-
+ *                         view rating is exact in bf16 (half-star ratings,
+ *                         rating - median: always), its row sums always;
+ *                         0: rhs on the VALU (fp32 FMAs in rating order) */
 enum { MR_OPT_FUSE_START = 0, MR_OPT_CG_SPECULATE = 1, MR_OPT_WAIT_TIMEOUT_S = 2,
-       MR_OPT_CG_ONEPASS = 3 };
+       MR_OPT_CG_ONEPASS = 3, MR_OPT_GRAM_RHS_MFMA = 4 };
 int mr_als_set_option(mr_als* ctx, int option, double value);
 /* Ratings per Gram work item: heavier entities are split across waves and
  * their partial normal equations combined in order.  Applies to contexts

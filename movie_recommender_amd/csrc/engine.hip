@@ -397,6 +397,15 @@ int Engine::init(int dev, int k_, int64_t U_, int64_t I_, int64_t n_u,
   MR_HIP(hipMemsetAsync(Ufac, 0, (U + 1) * ldk * 4, stream));
   MR_HIP(hipMemsetAsync(Ubias, 0, (U + 1) * 4, stream));
   MR_HIP(hipMemsetAsync(Vfac, 0, (I + 1) * ldk * 4, stream));
+  // user-side weights (the ratings as fp32) exact in bf16? -> the Gram may
+  // take the rhs on the matrix cores (MR_OPT_GRAM_RHS_MFMA)
+  w_bf16 = true;
+  for (int64_t t = 0; t < n_u && w_bf16; ++t) {
+    const float f = (float)uv_r[t];
+    uint32_t bits;
+    memcpy(&bits, &f, 4);
+    w_bf16 = (bits & 0xFFFFu) == 0;
+  }
   // upload + build both views
   const bool same = (uv_uid == iv_uid && uv_iid == iv_iid && uv_r == iv_r && n_u == n_i);
   for (int view = 0; view < (same ? 1 : 2); ++view) {
@@ -801,7 +810,8 @@ int Engine::gram(Side& S, bool start) {
   const int zrow = (int)(user ? I : U);
   const CgStart cs = cg_start_of(S);
   if (launch_gram(stream, user, k, S.work, S.n_work, S.idx, S.val, F, bias, zrow,
-                  direct_dst(S), slab_dst(S), start ? &cs : nullptr))
+                  direct_dst(S), slab_dst(S), start ? &cs : nullptr,
+                  user && rhs_mfma && w_bf16))
     return -1;
   if (toc(cls, -1, a)) return -1;
   if (S.n_split) {

@@ -707,17 +707,28 @@ __device__ __forceinline__ void gather_half(float (&f)[8][NB], float (&w)[8], Ch
 // 8 ratings (the 4 q-groups are combined in the epilogue); then the exact
 // 3-way split, packed 2 ratings per dword (rating 2j in the low half).
 template <int NB, bool USER>
-__device__ __forceinline__ void bf3_split(u32x4_t (&P)[3][NB], float (&cacc)[NB],
-                                          float (&sacc)[NB], float& wsum,
-                                          const float (&f)[8][NB], const float (&w)[8]) {
+__device__ __forceinline__ void bf3_split(u32x4_t (&P)[3][NB], u32x4_t& W, float (&cacc)[NB],
+                                          float& wsum, const float (&f)[8][NB],
+                                          const float (&w)[8], bool rhs_mfma) {
+  if (USER) {
+    // user side: the row sums (and, with bf16-exact weights, the rhs) are
+    // taken by the matrix cores as a 16-column block W (column 0: the
+    // weights, column 1: ones; gram_wave), whose B operand is built here
+    const int col = threadIdx.x & 15;
 #pragma unroll
-  for (int t = 0; t < 8; ++t) {
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      cacc[b] = fmaf(f[t][b], w[t], cacc[b]);
-      if (USER) sacc[b] += f[t][b];
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t wv = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, w[2 * j + 1]),
+                                                __builtin_bit_cast(uint32_t, w[2 * j]), 0x07060302u);
+      W[j] = col == 0 ? (rhs_mfma ? wv : 0u) : (col == 1 ? 0x3F803F80u : 0u);
     }
-    if (USER) wsum += w[t];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) wsum += w[t];
+  }
+  if (!USER || !rhs_mfma) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) cacc[b] = fmaf(f[t][b], w[t], cacc[b]);
   }
   // a = h + m + l per float: r = a - h, l = r - m (h, m = the value with its
   // low 16 bits cleared), then the bf16 pairs of ratings (2j, 2j+1) packed
@@ -775,13 +786,9 @@ __device__ __forceinline__ void mfma_entry_guard() {
 // the compiler makes for the epilogue -- depends on a statement at or after
 // the nops and cannot be scheduled between the last MFMA and them.
 template <int T>
-__device__ __forceinline__ void mfma_exit_guard(floatx4 (&acc)[T]) {
-  static_assert(T >= 4, "NB >= 5 only");
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3"
-               : "+a"(acc[0]), "+a"(acc[1]), "+a"(acc[2]), "+a"(acc[3]));
+__device__ __forceinline__ void acc_tie(floatx4 (&acc)[T], int g0) {
 #pragma unroll
-  for (int g = 4; g < T; g += 4) {
+  for (int g = g0; g < T; g += 4) {
     __builtin_amdgcn_sched_barrier(0);
     if (g + 3 < T)
       asm volatile("" : "+a"(acc[g]), "+a"(acc[g + 1]), "+a"(acc[g + 2]), "+a"(acc[g + 3]));
@@ -794,10 +801,19 @@ __device__ __forceinline__ void mfma_exit_guard(floatx4 (&acc)[T]) {
   }
   __builtin_amdgcn_sched_barrier(0);
 }
+template <int T, int TW>
+__device__ __forceinline__ void mfma_exit_guard(floatx4 (&acc)[T], floatx4 (&accw)[TW], bool w) {
+  static_assert(T >= 4, "NB >= 5 only");
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3"
+               : "+a"(acc[0]), "+a"(acc[1]), "+a"(acc[2]), "+a"(acc[3]));
+  acc_tie(acc, 4);
+  if (w) acc_tie(accw, 0);   // user side: the W block's accumulators too
+}
 
-template <int NB>
-__device__ __forceinline__ void bf3_mfma(floatx4 (&acc)[NB * (NB + 1) / 2],
-                                         const u32x4_t (&P)[3][NB]) {
+template <int NB, bool USER>
+__device__ __forceinline__ void bf3_mfma(floatx4 (&acc)[NB * (NB + 1) / 2], floatx4 (&accw)[NB],
+                                         const u32x4_t (&P)[3][NB], const u32x4_t& W) {
   if constexpr (NB >= 5) mfma_entry_guard();
 #pragma unroll
   for (int sidx = 0; sidx < 6; ++sidx) {
@@ -826,6 +842,23 @@ __device__ __forceinline__ void bf3_mfma(floatx4 (&acc)[NB * (NB + 1) / 2],
         ++t;
       }
   }
+  if constexpr (USER) {
+    // W block: D[m][0] += a[16 b + m] w (rhs), D[m][1] += a[16 b + m] (row
+    // sums); the weights are exact in bf16 (or zero), so the three parts of
+    // a give every product of weight >= 2^-16 of the fp32 ones
+#pragma unroll
+    for (int part = 0; part < 3; ++part)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        if constexpr (NB >= 5) {
+          asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(accw[b]) : "v"(P[part][b]), "v"(W));
+        } else {
+          accw[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8_t, P[part][b]), __builtin_bit_cast(bf16x8_t, W), accw[b],
+              0, 0, 0);
+        }
+      }
+  }
 }
 
 template <int NB, bool USER, bool FUSE, bool BUF>
@@ -834,7 +867,7 @@ __device__ __forceinline__ void gram_wave(
     const int32_t* __restrict__ idx, const float* __restrict__ val,
     const float* __restrict__ F, const float* __restrict__ bias, int k, int ldk, int zrow,
     const GramDst& direct, const GramDst& slab, const CgStart& cs, StartScratch<NB>* ssc,
-    double& drr, double& dpq, double& dqq) {
+    double& drr, double& dpq, double& dqq, bool rhs_mfma) {
   constexpr int T = NB * (NB + 1) / 2;
   const int lane = threadIdx.x & 63;
   // work-item fields in SGPRs: all control flow below is scalar
@@ -866,10 +899,14 @@ __device__ __forceinline__ void gram_wave(
   floatx4 acc[T];
 #pragma unroll
   for (int t = 0; t < T; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  floatx4 accw[NB];   // user side: the W block (rhs, row sums), see bf3_mfma
+#pragma unroll
+  for (int b = 0; b < NB; ++b) accw[b] = floatx4{0.f, 0.f, 0.f, 0.f};
   float cacc[NB], sacc[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b) { cacc[b] = 0.f; sacc[b] = 0.f; }
   float wsum = 0.f;
+  rhs_mfma = USER && rhs_mfma;
 
   // Main loop: one iteration = one 32-rating half with its own id / weight
   // registers (lanes 0..31; lanes 32..63 mirror them), so the loop body is
@@ -909,9 +946,9 @@ __device__ __forceinline__ void gram_wave(
   bias32(h0, 0);
   bias32(h1, 1);
   float Fr[8][NB], w[8];
-  u32x4_t P[3][NB];
+  u32x4_t P[3][NB], W;
   gather_half<NB, BUF>(Fr, w, fin32(h0, 0), src, row_bytes);
-  bf3_split<NB, USER>(P, cacc, sacc, wsum, Fr, w);
+  bf3_split<NB, USER>(P, W, cacc, wsum, Fr, w, rhs_mfma);
   // the last half is peeled: its iteration would gather and split a half
   // past the end (zero rows, weight 0) that no MFMA uses -- about one half's
   // VALU work per work item (users: ~6 halves each)
@@ -920,23 +957,40 @@ __device__ __forceinline__ void gram_wave(
     const ChunkRaw h3 = ld32(h + 3);
     bias32(h2, h + 2);
     gather_half<NB, BUF>(Fr, w, fin32(h1, h + 1), src, row_bytes);
-    bf3_mfma<NB>(acc, P);
+    bf3_mfma<NB, USER>(acc, accw, P, W);
     __builtin_amdgcn_sched_barrier(0);
-    bf3_split<NB, USER>(P, cacc, sacc, wsum, Fr, w);
+    bf3_split<NB, USER>(P, W, cacc, wsum, Fr, w, rhs_mfma);
     h1 = h2;
     h2 = h3;
   }
-  if (nhalves > 0) bf3_mfma<NB>(acc, P);
-  if constexpr (NB >= 5) mfma_exit_guard(acc);
+  if (nhalves > 0) bf3_mfma<NB, USER>(acc, accw, P, W);
+  if constexpr (NB >= 5) mfma_exit_guard(acc, accw, USER);
 
   // ---- epilogue -----------------------------------------------------------
+  // c and (user side) the row sums at virtual (b, col) in every lane: from
+  // the per-lane VALU partials (summed over the 4 rating groups q), or from
+  // the W block, whose D[4 q' + r][n] sits in lane (q', n) register r
+  // (n = 0: rhs, n = 1: row sums) -- lane (q, col) takes register col & 3
+  // of lane 16 (col >> 2) + n
+  if (USER) {
+    const int s0 = 16 * (col >> 2), r = col & 3;
 #pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    cacc[b] = xor_sum_f32<16>(cacc[b]);
-    cacc[b] = xor_sum_f32<32>(cacc[b]);
-    if (USER) {
-      sacc[b] = xor_sum_f32<16>(sacc[b]);
-      sacc[b] = xor_sum_f32<32>(sacc[b]);
+    for (int b = 0; b < NB; ++b) {
+      float v0[4], v1[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v0[j] = __shfl(accw[b][j], s0, 64);
+        v1[j] = __shfl(accw[b][j], s0 + 1, 64);
+      }
+      sacc[b] = r == 0 ? v1[0] : r == 1 ? v1[1] : r == 2 ? v1[2] : v1[3];
+      if (rhs_mfma) cacc[b] = r == 0 ? v0[0] : r == 1 ? v0[1] : r == 2 ? v0[2] : v0[3];
+    }
+  }
+  if (!rhs_mfma) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      cacc[b] = xor_sum_f32<16>(cacc[b]);
+      cacc[b] = xor_sum_f32<32>(cacc[b]);
     }
   }
   const bool to_slab = wslab >= 0;
@@ -1013,19 +1067,19 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 3 : 1)) void gram_kernel(
     const WorkItem* __restrict__ work, int64_t n_work,
     const int32_t* __restrict__ idx, const float* __restrict__ val,
     const float* __restrict__ F, const float* __restrict__ bias, int k, int ldk, int zrow,
-    GramDst direct, GramDst slab, CgStart cs) {
+    GramDst direct, GramDst slab, CgStart cs, int rhs_mfma) {
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t wi = (int64_t)blockIdx.x * GRAM_WAVES + wid;
   double drr = 0.0, dpq = 0.0, dqq = 0.0;
   if constexpr (!FUSE) {
     if (wi >= n_work) return;
     gram_wave<NB, USER, false, BUF>(wi, work, idx, val, F, bias, k, ldk, zrow, direct, slab, cs,
-                                    nullptr, drr, dpq, dqq);
+                                    nullptr, drr, dpq, dqq, rhs_mfma != 0);
   } else {
     __shared__ StartScratch<NB> scr[GRAM_WAVES];
     if (wi < n_work)
       gram_wave<NB, USER, true, BUF>(wi, work, idx, val, F, bias, k, ldk, zrow, direct, slab,
-                                     cs, &scr[wid], drr, dpq, dqq);
+                                     cs, &scr[wid], drr, dpq, dqq, rhs_mfma != 0);
     store_start_sums(drr, dpq, dqq, cs.parts);
   }
 }
@@ -1049,7 +1103,7 @@ template <int NB>
 static int launch_gram_nb(hipStream_t s, bool user_side, int k, const WorkItem* work,
                           int64_t n_work, const int32_t* idx, const float* val,
                           const float* F, const float* bias, int zrow, GramDst direct,
-                          GramDst slab, const CgStart* start) {
+                          GramDst slab, const CgStart* start, bool rhs_mfma) {
   if (n_work <= 0) return 0;
   const int64_t grid = (n_work + GRAM_WAVES - 1) / GRAM_WAVES;
   const CgStart cs = start ? *start : CgStart{};
@@ -1059,7 +1113,7 @@ static int launch_gram_nb(hipStream_t s, bool user_side, int k, const WorkItem* 
   const bool buf = BUFOK && (int64_t)(zrow + 1) * ldk_of(k) * 4 < ((int64_t)1 << 31);
 #define MR_GRAM_LAUNCH(U, FU, B)                                                          \
   MR_LAUNCH((gram_kernel<NB, U, FU, B>), dim3((unsigned)grid), dim3(256), 0, s, work, n_work, \
-            idx, val, F, bias, k, ldk_of(k), zrow, direct, slab, cs)
+            idx, val, F, bias, k, ldk_of(k), zrow, direct, slab, cs, rhs_mfma ? 1 : 0)
   if (buf) {
     if (user_side) {
       if (start) MR_GRAM_LAUNCH(true, true, BUFOK); else MR_GRAM_LAUNCH(true, false, BUFOK);
@@ -1348,7 +1402,7 @@ __global__ __launch_bounds__(256) void gram_largek_kernel(
 int launch_gram(hipStream_t s, bool user_side, int k, const WorkItem* work,
                 int64_t n_work, const int32_t* idx, const float* val,
                 const float* F, const float* bias, int zrow, GramDst direct,
-                GramDst slab, const CgStart* start) {
+                GramDst slab, const CgStart* start, bool rhs_mfma) {
   if (k > kMaxK) {
     MR_CHECK(start == nullptr, "k > 128: no fused CG start");
     MR_CHECK(k <= kMaxKLarge, "k > 512 not supported");
@@ -1386,7 +1440,7 @@ int launch_gram(hipStream_t s, bool user_side, int k, const WorkItem* work,
     return 0;
   }
 #define MR_GRAM_CASE(NB) \
-  case NB: return launch_gram_nb<NB>(s, user_side, k, work, n_work, idx, val, F, bias, zrow, direct, slab, start);
+  case NB: return launch_gram_nb<NB>(s, user_side, k, work, n_work, idx, val, F, bias, zrow, direct, slab, start, rhs_mfma);
   switch (nb16_of(k)) {
     MR_GRAM_CASE(1) MR_GRAM_CASE(2) MR_GRAM_CASE(3) MR_GRAM_CASE(4)
     MR_GRAM_CASE(5) MR_GRAM_CASE(6) MR_GRAM_CASE(7) MR_GRAM_CASE(8)
@@ -2365,6 +2419,21 @@ __global__ __launch_bounds__(256) void cg_update_kernel(
       pb[i] = -rv;
       acc = fma(rv, rv, acc);
     }
+  } else if (mode == UPD_FINISH) {
+    // the stopped one-pass solve's last x update only: its residual update
+    // would be dead (the next solve of this side starts from r0 = G x - c)
+    float4* x4 = reinterpret_cast<float4*>(x);
+    for (int64_t i = tid; i < n4; i += stride) {
+      float4 xv = x4[i];
+      const double2 pa = p2[2 * i], pb2 = p2[2 * i + 1];
+      xv.x = (float)fma(alpha, pa.x, (double)xv.x);
+      xv.y = (float)fma(alpha, pa.y, (double)xv.y);
+      xv.z = (float)fma(alpha, pb2.x, (double)xv.z);
+      xv.w = (float)fma(alpha, pb2.y, (double)xv.w);
+      x4[i] = xv;
+    }
+    for (int64_t i = tid; i < nb; i += stride) xb[i] = (float)fma(alpha, pb[i], (double)xb[i]);
+    return;
   } else {
     float4* x4 = reinterpret_cast<float4*>(x);
     for (int64_t i = tid; i < n4; i += stride) {

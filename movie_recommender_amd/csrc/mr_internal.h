@@ -242,12 +242,14 @@ enum CgUpd { UPD_INIT = 0, UPD_STEP = 1, UPD_FINISH = 2 };
 // F has zrow+1 rows; row zrow (and bias[zrow]) is all zero.
 // start != nullptr: every wave also starts the CG solve on its (unsplit)
 // entity -- r0 = Gx - c, p0 = -r0, q0 = G p0 -- and each block stores its
-// (r.r, p.Gp) pair to start->parts[2 * block]; split entities follow with
-// launch_cg_start_split after slab_reduce (pairs after the Gram blocks').
+// (r.r, p.Gp, q.q) triple to start->parts[3 * block]; split entities follow
+// with launch_cg_start_split after slab_reduce (triples after the Gram
+// blocks').  rhs_mfma (user side, MFMA Gram): every weight is exact in bf16,
+// so the rhs is taken by the matrix cores with the row sums (gram_wave).
 int launch_gram(hipStream_t s, bool user_side, int k, const WorkItem* work,
                 int64_t n_work, const int32_t* idx, const float* val,
                 const float* F, const float* bias, int zrow, GramDst direct,
-                GramDst slab, const CgStart* start = nullptr);
+                GramDst slab, const CgStart* start = nullptr, bool rhs_mfma = false);
 inline int64_t gram_blocks(int64_t n_work) { return (n_work + 3) / 4; }
 int launch_cg_start_split(hipStream_t s, bool user_side, int k, const SplitItem* split,
                           int64_t n_split, GramDst direct, const CgStart& cs, double* parts);

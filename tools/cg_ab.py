@@ -5,6 +5,7 @@ ALS iterations; reports per side the solve time per CG iteration (HIP-event
 span of the solve phase / M) and the per-class kernel means.
 
     python tools/cg_ab.py [--k 64] [--m 20] [--reps 3] [--onepass 0|1] [--tag NAME]
+                          [--opt gram_rhs_mfma=0 ...]
 (MR_LIB_PATH selects a variant library, tools/build_var.sh)"""
 import argparse
 import json
@@ -25,6 +26,8 @@ ap.add_argument("--m", type=int, default=20)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--onepass", type=int, default=1)
 ap.add_argument("--tag", default="")
+ap.add_argument("--opt", action="append", default=[],
+                help="engine option NAME=VALUE (engine.OPTIONS), repeatable")
 a = ap.parse_args()
 rs = load_data("ml-full", a.k)
 rng = np.random.RandomState(0)
@@ -34,6 +37,9 @@ out = {"tag": a.tag or os.environ.get("MR_LIB_PATH", "default"), "k": a.k, "m": 
        "onepass": a.onepass}
 with AlsContext(rs.user_ids, rs.item_ids, rs.ratings, a.k, rs.num_users, rs.num_items) as ctx:
     ctx.set_option("cg_onepass", a.onepass)
+    for o in a.opt:
+        name, val = o.split("=")
+        ctx.set_option(name, float(val))
     ctx.set_factors(U0, V0)
     ctx.iterate(3)
     ctx.sync()
