@@ -1963,8 +1963,15 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 4 : 2)) void cg_matvec_kernel(
 #ifndef MR_OP_OPAQUE
 #define MR_OP_OPAQUE 1
 #endif
+#ifndef MR_OP_WAVES
+#define MR_OP_WAVES 4
+#endif
 template <int NB, bool USER>
-__global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 : 4) : 2)) void cg_onepass_kernel(
+__global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 : MR_OP_WAVES) : 2))
+#ifdef MR_OP_WPE
+__attribute__((amdgpu_waves_per_eu(MR_OP_WPE, MR_OP_WPE)))
+#endif
+void cg_onepass_kernel(
     CgState* __restrict__ st, int update, int64_t E, int k, int ldk,
     const float* __restrict__ G, const float* __restrict__ Gs, const float* __restrict__ Gn,
     double* __restrict__ p, double* __restrict__ pb, double* __restrict__ r,

@@ -168,3 +168,30 @@ def test_cg_goldens_round3(name):
     assert it == int(d["iterations"])
     assert rel_err(x, d["x"]) < max(1e-10, 20 * float(d["tc_spread"]))
     assert abs(rr - float(d["final_rr"])) <= 1e-8 * max(1.0, float(d["final_rr"]))
+
+
+def test_scipy_path_restatement_solves_the_design_matrix():
+    """CPU: oracle/scipy_als (the reference's SciPy ALS path, timed as a CPU
+    baseline) solves the same design-matrix least squares as a dense lstsq
+    on a small well-posed case (users' rows [V_i, 1], movies' rows U_u[:k])."""
+    import numpy as np
+    from oracle import scipy_als
+    rng = np.random.default_rng(4)
+    nu, ni, k = 6, 5, 3
+    u = np.repeat(np.arange(nu), ni)
+    i = np.tile(np.arange(ni), nu)
+    r = rng.uniform(1, 5, len(u))
+    V = rng.uniform(-1, 1, ni * k)
+    x = scipy_als.solve_for_users(V, u, i, r, nu, k)
+    A = np.zeros((len(u), nu * (k + 1)))
+    for t in range(len(u)):
+        A[t, u[t] * (k + 1):u[t] * (k + 1) + k] = V.reshape(-1, k)[i[t]]
+        A[t, u[t] * (k + 1) + k] = 1.0
+    ref = np.linalg.lstsq(A, r, rcond=None)[0]
+    assert np.max(np.abs(x - ref)) < 1e-6
+    y = scipy_als.solve_for_movies(x, u, i, r, ni, k)
+    B = np.zeros((len(u), ni * k))
+    for t in range(len(u)):
+        B[t, i[t] * k:(i[t] + 1) * k] = x.reshape(-1, k + 1)[u[t], :k]
+    ref2 = np.linalg.lstsq(B, r - x[3::4][u], rcond=None)[0]
+    assert np.max(np.abs(y - ref2)) < 1e-6
