@@ -708,10 +708,15 @@ __device__ __forceinline__ void gather_half(float (&f)[8][NB], float (&w)[8], Ch
 // 3-way split, packed 2 ratings per dword (rating 2j in the low half).
 template <int NB, bool USER>
 __device__ __forceinline__ void bf3_split(u32x4_t (&P)[3][NB], u32x4_t& W, float (&cacc)[NB],
-                                          float& wsum, const float (&f)[8][NB],
-                                          const float (&w)[8], bool rhs_mfma) {
+                                          float (&sacc)[NB], float& wsum,
+                                          const float (&f)[8][NB], const float (&w)[8],
+                                          bool rhs_mfma) {
   if (USER) {
-    // user side: the row sums (and, with bf16-exact weights, the rhs) are
+#pragma unroll
+    for (int t = 0; t < 8; ++t) wsum += w[t];
+  }
+  if (rhs_mfma) {
+    // user side, every weight exact in bf16: the rhs and the row sums are
     // taken by the matrix cores as a 16-column block W (column 0: the
     // weights, column 1: ones; gram_wave), whose B operand is built here
     const int col = threadIdx.x & 15;
@@ -719,16 +724,17 @@ __device__ __forceinline__ void bf3_split(u32x4_t (&P)[3][NB], u32x4_t& W, float
     for (int j = 0; j < 4; ++j) {
       const uint32_t wv = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, w[2 * j + 1]),
                                                 __builtin_bit_cast(uint32_t, w[2 * j]), 0x07060302u);
-      W[j] = col == 0 ? (rhs_mfma ? wv : 0u) : (col == 1 ? 0x3F803F80u : 0u);
+      W[j] = col == 0 ? wv : (col == 1 ? 0x3F803F80u : 0u);
     }
+  } else {
 #pragma unroll
-    for (int t = 0; t < 8; ++t) wsum += w[t];
-  }
-  if (!USER || !rhs_mfma) {
+    for (int t = 0; t < 8; ++t) {
 #pragma unroll
-    for (int t = 0; t < 8; ++t)
-#pragma unroll
-      for (int b = 0; b < NB; ++b) cacc[b] = fmaf(f[t][b], w[t], cacc[b]);
+      for (int b = 0; b < NB; ++b) {
+        cacc[b] = fmaf(f[t][b], w[t], cacc[b]);
+        if (USER) sacc[b] += f[t][b];
+      }
+    }
   }
   // a = h + m + l per float: r = a - h, l = r - m (h, m = the value with its
   // low 16 bits cleared), then the bf16 pairs of ratings (2j, 2j+1) packed
@@ -813,7 +819,8 @@ __device__ __forceinline__ void mfma_exit_guard(floatx4 (&acc)[T], floatx4 (&acc
 
 template <int NB, bool USER>
 __device__ __forceinline__ void bf3_mfma(floatx4 (&acc)[NB * (NB + 1) / 2], floatx4 (&accw)[NB],
-                                         const u32x4_t (&P)[3][NB], const u32x4_t& W) {
+                                         const u32x4_t (&P)[3][NB], const u32x4_t& W,
+                                         bool rhs_mfma) {
   if constexpr (NB >= 5) mfma_entry_guard();
 #pragma unroll
   for (int sidx = 0; sidx < 6; ++sidx) {
@@ -842,10 +849,10 @@ __device__ __forceinline__ void bf3_mfma(floatx4 (&acc)[NB * (NB + 1) / 2], floa
         ++t;
       }
   }
-  if constexpr (USER) {
+  if (USER && rhs_mfma) {
     // W block: D[m][0] += a[16 b + m] w (rhs), D[m][1] += a[16 b + m] (row
-    // sums); the weights are exact in bf16 (or zero), so the three parts of
-    // a give every product of weight >= 2^-16 of the fp32 ones
+    // sums); the weights are exact in bf16, so the three parts of a give
+    // every product of weight >= 2^-16 of the fp32 ones
 #pragma unroll
     for (int part = 0; part < 3; ++part)
 #pragma unroll
@@ -948,7 +955,7 @@ __device__ __forceinline__ void gram_wave(
   float Fr[8][NB], w[8];
   u32x4_t P[3][NB], W;
   gather_half<NB, BUF>(Fr, w, fin32(h0, 0), src, row_bytes);
-  bf3_split<NB, USER>(P, W, cacc, wsum, Fr, w, rhs_mfma);
+  bf3_split<NB, USER>(P, W, cacc, sacc, wsum, Fr, w, rhs_mfma);
   // the last half is peeled: its iteration would gather and split a half
   // past the end (zero rows, weight 0) that no MFMA uses -- about one half's
   // VALU work per work item (users: ~6 halves each)
@@ -957,13 +964,13 @@ __device__ __forceinline__ void gram_wave(
     const ChunkRaw h3 = ld32(h + 3);
     bias32(h2, h + 2);
     gather_half<NB, BUF>(Fr, w, fin32(h1, h + 1), src, row_bytes);
-    bf3_mfma<NB, USER>(acc, accw, P, W);
+    bf3_mfma<NB, USER>(acc, accw, P, W, rhs_mfma);
     __builtin_amdgcn_sched_barrier(0);
-    bf3_split<NB, USER>(P, W, cacc, wsum, Fr, w, rhs_mfma);
+    bf3_split<NB, USER>(P, W, cacc, sacc, wsum, Fr, w, rhs_mfma);
     h1 = h2;
     h2 = h3;
   }
-  if (nhalves > 0) bf3_mfma<NB, USER>(acc, accw, P, W);
+  if (nhalves > 0) bf3_mfma<NB, USER>(acc, accw, P, W, rhs_mfma);
   if constexpr (NB >= 5) mfma_exit_guard(acc, accw, USER);
 
   // ---- epilogue -----------------------------------------------------------
@@ -972,7 +979,7 @@ __device__ __forceinline__ void gram_wave(
   // the W block, whose D[4 q' + r][n] sits in lane (q', n) register r
   // (n = 0: rhs, n = 1: row sums) -- lane (q, col) takes register col & 3
   // of lane 16 (col >> 2) + n
-  if (USER) {
+  if (rhs_mfma) {
     const int s0 = 16 * (col >> 2), r = col & 3;
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
@@ -983,14 +990,17 @@ __device__ __forceinline__ void gram_wave(
         v1[j] = __shfl(accw[b][j], s0 + 1, 64);
       }
       sacc[b] = r == 0 ? v1[0] : r == 1 ? v1[1] : r == 2 ? v1[2] : v1[3];
-      if (rhs_mfma) cacc[b] = r == 0 ? v0[0] : r == 1 ? v0[1] : r == 2 ? v0[2] : v0[3];
+      cacc[b] = r == 0 ? v0[0] : r == 1 ? v0[1] : r == 2 ? v0[2] : v0[3];
     }
-  }
-  if (!rhs_mfma) {
+  } else {
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       cacc[b] = xor_sum_f32<16>(cacc[b]);
       cacc[b] = xor_sum_f32<32>(cacc[b]);
+      if (USER) {
+        sacc[b] = xor_sum_f32<16>(sacc[b]);
+        sacc[b] = xor_sum_f32<32>(sacc[b]);
+      }
     }
   }
   const bool to_slab = wslab >= 0;
@@ -1062,24 +1072,24 @@ __device__ __forceinline__ void gram_wave(
 // the FUSE form, whose waves then start the CG solve on their entity
 // (start_from_acc; split entities are started after slab_reduce) and meet
 // once at the end to store the block's (r.r, p.Gp) pair.
-template <int NB, bool USER, bool FUSE, bool BUF>
+template <int NB, bool USER, bool FUSE, bool BUF, bool RHSM>
 __global__ __launch_bounds__(256, (NB <= 4 ? 3 : 1)) void gram_kernel(
     const WorkItem* __restrict__ work, int64_t n_work,
     const int32_t* __restrict__ idx, const float* __restrict__ val,
     const float* __restrict__ F, const float* __restrict__ bias, int k, int ldk, int zrow,
-    GramDst direct, GramDst slab, CgStart cs, int rhs_mfma) {
+    GramDst direct, GramDst slab, CgStart cs) {
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t wi = (int64_t)blockIdx.x * GRAM_WAVES + wid;
   double drr = 0.0, dpq = 0.0, dqq = 0.0;
   if constexpr (!FUSE) {
     if (wi >= n_work) return;
     gram_wave<NB, USER, false, BUF>(wi, work, idx, val, F, bias, k, ldk, zrow, direct, slab, cs,
-                                    nullptr, drr, dpq, dqq, rhs_mfma != 0);
+                                    nullptr, drr, dpq, dqq, RHSM);
   } else {
     __shared__ StartScratch<NB> scr[GRAM_WAVES];
     if (wi < n_work)
       gram_wave<NB, USER, true, BUF>(wi, work, idx, val, F, bias, k, ldk, zrow, direct, slab,
-                                     cs, &scr[wid], drr, dpq, dqq, rhs_mfma != 0);
+                                     cs, &scr[wid], drr, dpq, dqq, RHSM);
     store_start_sums(drr, dpq, dqq, cs.parts);
   }
 }
@@ -1111,22 +1121,25 @@ static int launch_gram_nb(hipStream_t s, bool user_side, int k, const WorkItem* 
   // and the row segment is whole dwordx4s (NB = 4, 8)
   constexpr bool BUFOK = NB % 4 == 0;
   const bool buf = BUFOK && (int64_t)(zrow + 1) * ldk_of(k) * 4 < ((int64_t)1 << 31);
-#define MR_GRAM_LAUNCH(U, FU, B)                                                          \
-  MR_LAUNCH((gram_kernel<NB, U, FU, B>), dim3((unsigned)grid), dim3(256), 0, s, work, n_work, \
-            idx, val, F, bias, k, ldk_of(k), zrow, direct, slab, cs, rhs_mfma ? 1 : 0)
+#define MR_GRAM_LAUNCH(U, FU, B, R)                                                          \
+  MR_LAUNCH((gram_kernel<NB, U, FU, B, R>), dim3((unsigned)grid), dim3(256), 0, s, work, n_work, \
+            idx, val, F, bias, k, ldk_of(k), zrow, direct, slab, cs)
+#define MR_GRAM_USER(FU, B)                                                                 \
+  if (rhs_mfma) MR_GRAM_LAUNCH(true, FU, B, true); else MR_GRAM_LAUNCH(true, FU, B, false);
   if (buf) {
     if (user_side) {
-      if (start) MR_GRAM_LAUNCH(true, true, BUFOK); else MR_GRAM_LAUNCH(true, false, BUFOK);
+      if (start) { MR_GRAM_USER(true, BUFOK) } else { MR_GRAM_USER(false, BUFOK) }
     } else {
-      if (start) MR_GRAM_LAUNCH(false, true, BUFOK); else MR_GRAM_LAUNCH(false, false, BUFOK);
+      if (start) MR_GRAM_LAUNCH(false, true, BUFOK, false); else MR_GRAM_LAUNCH(false, false, BUFOK, false);
     }
   } else {
     if (user_side) {
-      if (start) MR_GRAM_LAUNCH(true, true, false); else MR_GRAM_LAUNCH(true, false, false);
+      if (start) { MR_GRAM_USER(true, false) } else { MR_GRAM_USER(false, false) }
     } else {
-      if (start) MR_GRAM_LAUNCH(false, true, false); else MR_GRAM_LAUNCH(false, false, false);
+      if (start) MR_GRAM_LAUNCH(false, true, false, false); else MR_GRAM_LAUNCH(false, false, false, false);
     }
   }
+#undef MR_GRAM_USER
 #undef MR_GRAM_LAUNCH
   MR_HIP(hipGetLastError());
   return 0;

@@ -231,12 +231,16 @@ def test_replay_from_snapshot_is_bitwise_identical(gpu):
         assert np.array_equal(U, U1) and np.array_equal(V, V1)
 
 
+@pytest.mark.parametrize("ratings", ["normal", "halfstar"])
 @pytest.mark.parametrize("k", [3, 10, 16, 20, 32, 33, 64, 65, 96, 128, 144, 200, 300])
-def test_gram_kernel_vs_numpy(gpu, k):
+def test_gram_kernel_vs_numpy(gpu, k, ratings):
     """Normal equations of both sides against fp64 NumPy -- VALU fp32 for
     k < 32, bf16x3 split on the bf16 MFMA for 32 <= k <= 128, the streamed
     large-k kernel above -- including heavy entities split across waves
-    (chunk 64 forces slabs) and empty entities."""
+    (chunk 64 forces slabs) and empty entities.  "halfstar" ratings
+    (rating - median style, exact in bf16) take the user-side rhs through
+    the MFMA W block; "normal" ones keep it on the VALU (row sums on the
+    MFMA either way)."""
     from movie_recommender_amd.engine import AlsContext
     from oracle import als_oracle as O
     rng = np.random.default_rng(k)
@@ -247,7 +251,7 @@ def test_gram_kernel_vs_numpy(gpu, k):
     key = np.unique(u.astype(np.int64) * nI + i)
     u = (key // nI).astype(np.int32)
     i = (key % nI).astype(np.int32)
-    r = rng.normal(0, 1, len(u))
+    r = rng.normal(0, 1, len(u)) if ratings == "normal" else rng.integers(1, 11, len(u)) / 2.0 - 3.25
     U0 = rng.uniform(-1, 1, nU * (k + 1))
     V0 = rng.uniform(-1, 1, nI * k)
     with AlsContext(u, i, r, k, nU, nI, gram_chunk=64) as ctx:
@@ -321,6 +325,39 @@ def test_cg_iterations_vs_oracle(gpu, k, fuse, chunk, onepass):
                         (side, m, np.max(np.abs(got - x)), step)
     finally:
         _lib.check(_lib.lib().mr_set_gram_chunk(2048), "reset chunk")
+
+
+def test_gram_rhs_path_selection(gpu):
+    """The user-side rhs goes through the MFMA W block only when every rating
+    is exact in bf16 (and the option is on): with half-star ratings the two
+    settings give different roundings of c (both within 2e-5 of fp64), with
+    arbitrary ratings the option changes nothing (bitwise)."""
+    from movie_recommender_amd.engine import AlsContext
+    from oracle import als_oracle as O
+    k, nU, nI = 64, 60, 80
+    rng = np.random.default_rng(11)
+    key = np.unique(rng.integers(0, nU, 3000) * nI + rng.integers(0, nI, 3000))
+    u = (key // nI).astype(np.int32)
+    i = (key % nI).astype(np.int32)
+    V0 = rng.uniform(-1, 1, nI * k)
+    U0 = rng.uniform(-1, 1, nU * (k + 1))
+    for kind, r in (("halfstar", rng.integers(1, 11, len(u)) / 2.0 - 3.0),
+                    ("normal", rng.normal(0, 1, len(u)))):
+        Gf, cf = O.gram_user(u, i, r, V0, k, nU)
+        cs = {}
+        for on in (1, 0):
+            with AlsContext(u, i, r, k, nU, nI) as ctx:
+                ctx.set_option("gram_rhs_mfma", on)
+                ctx.set_factors(U0, V0)
+                ctx.build_normal_equations("users")
+                G, c = ctx.normal_equations("users", np.arange(nU))
+            scale = np.maximum(np.abs(cf).max(axis=1), 1.0)
+            assert np.max(np.abs(c - cf).max(axis=1) / scale) < 2e-5, (kind, on)
+            cs[on] = c
+        if kind == "halfstar":
+            assert not np.array_equal(cs[1], cs[0])
+        else:
+            assert np.array_equal(cs[1], cs[0])
 
 
 def test_split_vs_unsplit_same_result(gpu):
