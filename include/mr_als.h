@@ -165,11 +165,12 @@ int mr_als_set_timing(mr_als* ctx, int enable);
  *                         the next matvec, r'.r' from r.r, r.q, q.q; k <= 128,
  *                         unsharded or peer scalars, not the user side at
  *                         k > 64); 0: matvec + update
- *   MR_OPT_GRAM_RHS_MFMA  1 (default): the user-side Gram (32 <= k <= 128)
- *                         takes its rhs on the matrix cores when every user-
- *                         view rating is exact in bf16 (half-star ratings,
- *                         rating - median: always), its row sums always;
- *                         0: rhs on the VALU (fp32 FMAs in rating order) */
+ *   MR_OPT_GRAM_RHS_MFMA  1 (default): the user-side Gram at 64 < k <= 128
+ *                         takes its rhs and row sums on the matrix cores when
+ *                         every user-view rating is exact in bf16 (half-star
+ *                         ratings, rating - median: always; measured -4 % at
+ *                         k = 128, level at k = 64, where the VALU path
+ *                         stays); 0: always on the VALU (fp32, rating order) */
 enum { MR_OPT_FUSE_START = 0, MR_OPT_CG_SPECULATE = 1, MR_OPT_WAIT_TIMEOUT_S = 2,
        MR_OPT_CG_ONEPASS = 3, MR_OPT_GRAM_RHS_MFMA = 4 };
 int mr_als_set_option(mr_als* ctx, int option, double value);

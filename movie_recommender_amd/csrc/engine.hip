@@ -811,7 +811,7 @@ int Engine::gram(Side& S, bool start) {
   const CgStart cs = cg_start_of(S);
   if (launch_gram(stream, user, k, S.work, S.n_work, S.idx, S.val, F, bias, zrow,
                   direct_dst(S), slab_dst(S), start ? &cs : nullptr,
-                  user && rhs_mfma && w_bf16))
+                  user && rhs_mfma && w_bf16 && nb16_of(k) >= 5))
     return -1;
   if (toc(cls, -1, a)) return -1;
   if (S.n_split) {
