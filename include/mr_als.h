@@ -130,6 +130,10 @@ int mr_als_set_rccl(mr_als* ctx, const unsigned char id[128], int rank, int worl
 int mr_als_peer_handle(mr_als* ctx, unsigned char out[64]);
 int mr_als_set_peer(mr_als* ctx, const unsigned char* handles, int rank, int world);
 int mr_als_peer_selftest(mr_als* ctx);
+/* Latency probe of the peer all-reduce (collective, same iters on every
+ * rank): `iters` reductions of one double back to back by one device thread;
+ * *us = mean microseconds per reduction (HIP events around the kernel). */
+int mr_als_peer_latency(mr_als* ctx, int iters, double* us);
 
 void mr_als_destroy(mr_als* ctx);
 

@@ -233,6 +233,11 @@ int mr_als_peer_selftest(mr_als* ctx) {
   return guarded([&]() { return ctx->eng.peer_selftest(); });
 }
 
+int mr_als_peer_latency(mr_als* ctx, int iters, double* us) {
+  MR_CHECK(ctx && us, "null argument");
+  return guarded([&]() { return ctx->eng.peer_latency(iters, us); });
+}
+
 void mr_als_destroy(mr_als* ctx) { delete ctx; }
 
 int mr_als_set_factors(mr_als* ctx, const double* U, const double* V) {

@@ -127,6 +127,7 @@ struct Engine {
   int peer_handle(unsigned char* out64);
   int set_peer(const unsigned char* handles, int rank, int world);
   int peer_selftest();
+  int peer_latency(int iters, double* us);
   // padded all-gather staging (both transports): every shard padded to the
   // largest one; needs row_begin_u / row_begin_i
   int alloc_ag(int world);

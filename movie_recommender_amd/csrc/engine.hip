@@ -607,6 +607,35 @@ int Engine::peer_selftest() {
   return 0;
 }
 
+// Device-side latency of the peer all-reduce (collective: every rank calls it
+// with the same iters): mean microseconds per reduction over `iters`
+// back-to-back reductions by one thread, from HIP events around the kernel.
+int Engine::peer_latency(int iters, double* us) {
+  MR_CHECK(peer_on && d_peer, "peer all-reduce not set up");
+  MR_CHECK(iters >= 1 && iters <= 1000000, "iters must be in [1, 1e6]");
+  MR_HIP(hipSetDevice(device));
+  double* d_out = nullptr;
+  if (dalloc(&d_out, 2, stream)) return -1;
+  hipEvent_t a, b;
+  MR_HIP(hipEventCreate(&a));
+  MR_HIP(hipEventCreate(&b));
+  MR_HIP(hipEventRecord(a, stream));
+  int rc = launch_peer_bench(stream, d_peer, iters, d_out);
+  MR_HIP(hipEventRecord(b, stream));
+  double out[2] = {0, 0};
+  if (!rc) rc = t_stager.d2h(stream, out, d_out, sizeof(out));
+  float ms = 0.f;
+  MR_HIP(hipEventSynchronize(b));
+  MR_HIP(hipEventElapsedTime(&ms, a, b));
+  MR_HIP(hipEventDestroy(a));
+  MR_HIP(hipEventDestroy(b));
+  dfree(d_out, stream);
+  if (rc) return -1;
+  MR_CHECK(out[0] == 1.0 && out[1] == iters, "peer all-reduce latency probe: wrong sum or timeout");
+  *us = 1e3 * ms / iters;
+  return 0;
+}
+
 // All-gather staging, the same for both transports: every rank's shard padded
 // to the largest one (maxrows rows of ldk floats, + the user bias column).
 // Row boundaries are checked here, on the host, against everything the pack /

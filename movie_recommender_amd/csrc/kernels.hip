@@ -1709,6 +1709,27 @@ __global__ void peer_selftest_kernel(PeerComm* pc, double* out) {
   out[2] = ok ? 1.0 : 0.0;
 }
 
+// Latency probe: `iters` back-to-back reductions of one value by one thread
+// (the finalizing thread's part of a CG iteration); out = {ok, iters done}.
+__global__ void peer_bench_kernel(PeerComm* pc, int iters, double* out) {
+  if (threadIdx.x != 0) return;
+  const double want = 0.5 * pc->world * (pc->world + 1);
+  int ok = 1, n = 0;
+  for (; n < iters; ++n) {
+    double v = (double)(pc->rank + 1);
+    if (!peer_sum(pc, &v, 1)) { ok = 0; break; }
+    if (v != want) ok = 0;
+  }
+  out[0] = ok;
+  out[1] = n;
+}
+
+int launch_peer_bench(hipStream_t s, PeerComm* pc, int iters, double* out) {
+  peer_bench_kernel<<<1, 64, 0, s>>>(pc, iters, out);
+  MR_HIP(hipGetLastError());
+  return 0;
+}
+
 int launch_peer_selftest(hipStream_t s, PeerComm* pc, double* out) {
   peer_selftest_kernel<<<1, 64, 0, s>>>(pc, out);
   MR_HIP(hipGetLastError());

@@ -191,6 +191,8 @@ struct PeerComm {
 
 // One peer reduction of {rank + 1, 1} into out[0..2] = {sum, count, ok}.
 int launch_peer_selftest(hipStream_t s, PeerComm* pc, double* out);
+// `iters` reductions of one value back to back; out = {ok, iters done}.
+int launch_peer_bench(hipStream_t s, PeerComm* pc, int iters, double* out);
 
 // CG scalar state, device resident (matrix.cpp:456-529 scalars).
 struct CgState {

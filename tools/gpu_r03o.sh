@@ -27,4 +27,7 @@ step c5 900 python -u bench.py --no-cpu --shape c5 --scale 0.125 --k 128 --steps
 cut -c1-300 $OUT/bench_c5_slice_k128.json
 step shard_peer 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --no-cpu --steps 20 --warmup 3 --force-shard --scalars peer > $OUT/bench_shard1_peer.json 2> $OUT/bench_shard1_peer.err
 step shard_coll 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29512 bench.py --no-cpu --steps 20 --warmup 3 --force-shard --scalars collective > $OUT/bench_shard1_coll.json 2> $OUT/bench_shard1_coll.err
+step peer2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29513 tools/peer_latency.py > $OUT/peer_latency_w2.json 2> $OUT/peer_latency_w2.err
+step peer3 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 3 --master-addr 127.0.0.1 --master-port 29514 tools/peer_latency.py > $OUT/peer_latency_w3.json 2> $OUT/peer_latency_w3.err
+cat $OUT/peer_latency_w2.json $OUT/peer_latency_w3.json
 echo DONE
