@@ -250,6 +250,11 @@ int mr_als_predict(mr_als* ctx, long long n, const int* user_ids,
  * ldk must be a multiple of 4; shapes are checked on the host first. */
 int mr_test_pack_rows(int device, long long rows, int ldk, const float* fac, const float* bias,
                       long long r0, long long n, float* send, float* send_b);
+/* Test hook: the one-pass CG's order-independent sum (an exact integer sum of
+ * the terms truncated to multiples of 2^-192, converted to fp64) of n terms
+ * dealt to the waves of `blocks` blocks; *out = the sum (NaN if a term is not
+ * finite or >= 2^96 in magnitude). */
+int mr_test_xsum(int device, const double* terms, long long n, int blocks, double* out);
 int mr_test_unstage_rows(int device, int world, int skip, const long long* rb, long long maxrows,
                          int ldk, const float* recv, const float* recv_b, float* fac,
                          float* bias);

@@ -150,6 +150,7 @@ SIGNATURES = {
     "mr_als_predict": (ctypes.c_int, [VP, ctypes.c_longlong, IP, IP, DP]),
     "mr_test_pack_rows": (ctypes.c_int, [ctypes.c_int, ctypes.c_longlong, ctypes.c_int, FP, FP,
                                          ctypes.c_longlong, ctypes.c_longlong, FP, FP]),
+    "mr_test_xsum": (ctypes.c_int, [ctypes.c_int, DP, ctypes.c_longlong, ctypes.c_int, DP]),
     "mr_test_unstage_rows": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, LLP,
                                             ctypes.c_longlong, ctypes.c_int, FP, FP, FP, FP]),
     # general sparse least squares (include/mr_cg.h)
@@ -210,6 +211,8 @@ def lib():
             " or `make -C movie_recommender_amd/csrc`")
     L = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
+        if os.environ.get("MR_LIB_PATH") and not hasattr(L, name):
+            continue  # an older A/B variant (tools/build_var.sh) lacks newer entry points
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

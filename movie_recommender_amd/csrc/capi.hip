@@ -448,6 +448,24 @@ int mr_test_pack_rows(int device, long long rows, int ldk, const float* fac, con
   });
 }
 
+int mr_test_xsum(int device, const double* terms, long long n, int blocks, double* out) {
+  return guarded([&]() -> int {
+    MR_CHECK(n >= 0 && blocks >= 1 && blocks <= 65535 && out, "bad arguments");
+    MR_HIP(hipSetDevice(device));
+    DevScratch d;
+    MR_HIP(hipStreamCreateWithFlags(&d.s, hipStreamNonBlocking));
+    double *dt, *dout;
+    int64_t* bins;
+    if (d.alloc(&dt, std::max<long long>(n, 1)) || d.alloc(&dout, 1) || d.alloc(&bins, 16 * 11))
+      return -1;
+    MR_HIP(hipMemsetAsync(bins, 0, 16 * 11 * 8, d.s));
+    if (n) MR_H2D(dt, terms, n * 8, d.s);
+    if (mr::launch_xsum_test(d.s, dt, n, blocks, bins, dout)) return -1;
+    MR_D2H(out, dout, 8, d.s);
+    return 0;
+  });
+}
+
 int mr_test_unstage_rows(int device, int world, int skip, const long long* rb, long long maxrows,
                          int ldk, const float* recv, const float* recv_b, float* fac,
                          float* bias) {

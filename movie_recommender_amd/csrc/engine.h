@@ -73,6 +73,9 @@ struct Engine {
   CgMirror* d_mirror = nullptr;   // its device address
   int mirror_seq = 0;
   double* partials = nullptr;
+  // bins of the one-pass CG's order-independent sums: kXBinWords for the
+  // iteration kernel, then 16 x 3 x 11 for the fused start (kernels.hip)
+  int64_t* xbins = nullptr;
   int* d_flag = nullptr;
   int cur_parts = 1;
   int solver = MR_SOLVER_CG;
@@ -142,6 +145,8 @@ struct Engine {
   int gram(Side& S, bool start = false);
   int x_ptrs(Side& S, float** xf, float** xb);
   int cg(Side& S, double min_dec, int max_it, double* final_rr, bool started = false);
+  // the one-pass CG iteration runs this side's solve (Engine::cg)
+  bool onepass_for(const Side& S) const;
   int cg_onepass(Side& S, double min_dec, int max_it, double* final_rr, bool started);
   CgStart cg_start_of(Side& S);
   int solve(Side& S);

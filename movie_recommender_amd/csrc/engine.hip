@@ -75,7 +75,7 @@ Engine::~Engine() {
       dfree(A->send, stream); dfree(A->recv, stream); dfree(A->send_b, stream);
       dfree(A->recv_b, stream); dfree(A->rb, stream);
     }
-    dfree(d_state, stream); dfree(partials, stream); dfree(d_flag, stream);
+    dfree(d_state, stream); dfree(partials, stream); dfree(d_flag, stream); dfree(xbins, stream);
     dfree(d_peer, stream);
     for (void* q : peer_opened) (void)hipIpcCloseMemHandle(q);
     if (peer_buf) (void)hipFree(peer_buf);
@@ -382,8 +382,9 @@ int Engine::init(int dev, int k_, int64_t U_, int64_t I_, int64_t n_u,
   memset(h_mirror, 0, kMirrorSlots * sizeof(CgMirror));
   MR_HIP(hipHostGetDevicePointer((void**)&d_mirror, h_mirror, 0));
   if (dalloc(&d_state, 1, stream) || dalloc(&partials, 4 * kMaxParts, stream) ||
-      dalloc(&d_flag, 4, stream))
+      dalloc(&d_flag, 4, stream) || dalloc(&xbins, kXBinWords + kXBinStartWords, stream))
     return -1;
+  MR_HIP(hipMemsetAsync(xbins, 0, (kXBinWords + kXBinStartWords) * sizeof(int64_t), stream));
   // every field defined before any kernel reads it: the fused CG start
   // re-initialises the scalars but not `peer` (set only by set_peer)
   MR_HIP(hipMemsetAsync(d_state, 0, sizeof(CgState), stream));
@@ -824,7 +825,17 @@ CgStart Engine::cg_start_of(Side& S) {
   cs.xb = xb;
   cs.r = S.r; cs.rb = S.rb; cs.p = S.p; cs.pb = S.pb; cs.q = S.q; cs.qb = S.qb;
   cs.parts = S.start_parts;
+  cs.xbins = onepass_for(S) ? xbins + kXBinWords : nullptr;
   return cs;
+}
+
+bool Engine::onepass_for(const Side& S) const {
+  // one pass per CG iteration everywhere except the user side at k > 64:
+  // there the one-pass kernel (32 tiles + the deferred-update vectors at 2
+  // waves / SIMD) spills 18 registers and measured 3 % slower per CG
+  // iteration than matvec + update (k = 128, ML-full, fixed 20 iterations:
+  // 0.286 vs 0.278 ms); the item side gains 8 % there
+  return onepass && k <= kMaxK && (!S.user || nb16_of(k) <= 4) && (!sharded() || peer_on);
 }
 
 // start: the Gram waves also start the CG solve (r0, p0, q0 = G p0 and the
@@ -870,12 +881,7 @@ int Engine::x_ptrs(Side& S, float** xf, float** xb) {
 // that t cannot terminate (fails == 0, rr far above 1e-6, t+1 < max_it) --
 // so the stream stays busy without launching iterations that would be idle.
 int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr, bool started) {
-  // one pass per CG iteration everywhere except the user side at k > 64:
-  // there the one-pass kernel (32 tiles + the deferred-update vectors at 2
-  // waves / SIMD) spills 18 registers and measured 3 % slower per CG
-  // iteration than matvec + update (k = 128, ML-full, fixed 20 iterations:
-  // 0.286 vs 0.278 ms); the item side gains 13 % there
-  if (onepass && k <= kMaxK && (!S.user || nb16_of(k) <= 4) && (!sharded() || peer_on))
+  if (onepass_for(S))
     return cg_onepass(S, min_dec, max_it, final_rr, started);
   float *xf, *xb;
   x_ptrs(S, &xf, &xb);
@@ -1076,7 +1082,8 @@ int Engine::cg_onepass(Side& S, double min_dec, int max_it, double* final_rr, bo
     seq_of.push_back(++mirror_seq);
     if (tic(MR_K_CG_CONTROL, -1, &a)) return -1;
     if (launch_cg_control(stream, d_state, CG_START, CTL_BOTH, S.start_parts,
-                          (int)S.n_start_pairs, d_mirror, seq_of[0], min_dec, max_it, 2))
+                          (int)S.n_start_pairs, d_mirror, seq_of[0], min_dec, max_it, 2,
+                          xbins + kXBinWords))
       return -1;
     if (toc(MR_K_CG_CONTROL, -1, a)) return -1;
     launched = 1;
@@ -1103,7 +1110,7 @@ int Engine::cg_onepass(Side& S, double min_dec, int max_it, double* final_rr, bo
     hipEvent_t ev = nullptr;
     if (tic(mv_cls, t, &ev)) return -1;
     if (launch_cg_onepass(stream, user, d_state, t > 0 ? 1 : 0, S.E, k, S.G, S.Gs, S.Gn, S.p,
-                          S.pb, S.r, S.rb, S.q, S.qb, xf, xb, partials, S.n_part_op, d_mirror,
+                          S.pb, S.r, S.rb, S.q, S.qb, xf, xb, xbins, S.n_part_op, d_mirror,
                           seq_of.back()))
       return -1;
     return toc(mv_cls, t, ev);

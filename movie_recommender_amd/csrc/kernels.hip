@@ -79,6 +79,129 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
   v += dpp_f64<0x4E>(v);
   return v + dpp_f64<0xB1>(v);
 }
+// ---------------------------------------------------------------------------
+// Order-independent CG sums (round 3; the one-pass CG and its fused start).
+// A sum of fp64 terms is kept as an integer: every term is truncated toward
+// zero to a multiple of 2^kXLsb and added exactly into kXD 32-bit digits held
+// in int64 containers (digit j weighs 2^(32 j + kXLsb); a term adds < 2^32 to
+// at most three digits, so 2^31 terms fit without a carry).  Integer
+// addition is associative: the value does not depend on which lane, wave,
+// block or rank added which term, so a sharded run (or another grid size)
+// reproduces the scalars bit for bit.  Digit kXD counts terms that are not
+// finite or >= 2^96 in magnitude (the sum is then NaN; the CG's sums are
+// far below that).  Lane j < kXD of a wave holds digit j, lane kXD the count.
+// ---------------------------------------------------------------------------
+constexpr int kXD = 10;
+constexpr int kXLsb = -192;
+constexpr int kXW = kXD + 1;   // containers per sum (digits + the count)
+
+__device__ __forceinline__ int64_t xterm(double t, int j) {
+  const uint64_t bits = (uint64_t)__double_as_longlong(t);
+  const int e = (int)((bits >> 52) & 0x7FF);
+  uint64_t m = bits & 0xFFFFFFFFFFFFFull;
+  int x = -1074;
+  if (e != 0) {
+    m |= 1ull << 52;
+    x = e - 1075;
+  }
+  if (j == kXD) return (e == 0x7FF || x + 53 > 96) ? 1 : 0;
+  if (e == 0x7FF || x + 53 > 96) return 0;
+  int p = x - kXLsb;
+  if (p < 0) {
+    m = p <= -64 ? 0 : (m >> (-p));
+    p = 0;
+  }
+  const int i = p >> 5, o = p & 31;
+  const uint64_t lo = m << o, hi = o ? (m >> (64 - o)) : 0;
+  int64_t v = 0;
+  if (j == i) v = (int64_t)(lo & 0xFFFFFFFFull);
+  else if (j == i + 1) v = (int64_t)(lo >> 32);
+  else if (j == i + 2) v = (int64_t)hi;
+  return (bits >> 63) ? -v : v;
+}
+
+// Canonical digits (carries propagated) -> fp64, the same operations in the
+// same order everywhere (tests/test_oracle.py restates it): Horner in base
+// 2^32 from the top digit, then the exact scaling by 2^kXLsb.
+__device__ double xsum_value(const int64_t* c_in) {
+  if (c_in[kXD] != 0) return __longlong_as_double(0x7FF8000000000000ll);
+  int64_t c[kXD];
+#pragma unroll
+  for (int j = 0; j < kXD; ++j) c[j] = c_in[j];
+#pragma unroll
+  for (int j = 0; j < kXD - 1; ++j) {
+    const int64_t carry = c[j] >> 32;   // floor division by 2^32
+    c[j] -= carry * 4294967296ll;
+    c[j + 1] += carry;
+  }
+  double v = (double)c[kXD - 1];
+#pragma unroll
+  for (int j = kXD - 2; j >= 0; --j) v = __dadd_rn(__dmul_rn(v, 4294967296.0), (double)c[j]);
+  return ldexp(v, kXLsb);
+}
+
+// Block-level flush of each wave's per-lane containers of NV sums into the
+// global bins [kXBins][NV][kXW] (bin = block mod kXBins, agent-scope integer
+// atomics: exact, so their order does not matter).
+constexpr int kXBins = 16;
+// Entities per term of the one-pass CG's sums (a function of the kernel
+// variant only, never of the grid or the shard): larger chunks save wave
+// sums, smaller ones shorten the last round of a wave's entities.  Shard
+// boundaries at multiples of kXAlign (distributed.SUM_CHUNK) keep a sharded
+// run's terms those of the single-GPU run.
+#ifndef MR_XC_U
+#define MR_XC_U 4
+#endif
+#ifndef MR_XC_I
+#define MR_XC_I 2
+#endif
+constexpr int kXAlign = 4;
+constexpr int xchunk_of(int nb, bool user) { return nb > 4 ? 1 : (user ? MR_XC_U : MR_XC_I); }
+static_assert(kXAlign % MR_XC_U == 0 && kXAlign % MR_XC_I == 0, "chunks must divide kXAlign");
+// The block's containers in LDS, sh[nsh][sum][container] (one set per wave,
+// or one per block).
+template <int NV>
+__device__ __forceinline__ void xsum_flush_lds(int64_t (*sh)[NV][kXW], int64_t* __restrict__ bins,
+                                               int nsh) {
+  __syncthreads();
+  if (threadIdx.x < NV * kXW) {
+    const int v = threadIdx.x / kXW, d = threadIdx.x % kXW;
+    int64_t t = 0;
+    for (int w = 0; w < nsh; ++w) t += sh[w][v][d];
+    if (t != 0)
+      __hip_atomic_fetch_add(bins + ((int64_t)(blockIdx.x % kXBins) * NV + v) * kXW + d, t,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+template <int NV>
+__device__ __forceinline__ void xsum_flush(const int64_t (&acc)[NV], int64_t* __restrict__ bins) {
+  __shared__ int64_t sh[4][NV][kXW];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane < kXW) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) sh[wid][v][lane] = acc[v];
+  }
+  xsum_flush_lds<NV>(sh, bins, (int)(blockDim.x >> 6));
+}
+
+// The consumer, one wave (of the last block / control): lane l < NV * kXW
+// returns the bins' total of container l (sum v = l / kXW, digit l % kXW)
+// and resets those bins for the next kernel (stream order).
+template <int NV>
+__device__ __forceinline__ int64_t xsum_collect(int64_t* __restrict__ bins, int lane) {
+  int64_t t = 0;
+  if (lane < NV * kXW) {
+    const int v = lane / kXW, d = lane % kXW;
+#pragma unroll
+    for (int b = 0; b < kXBins; ++b) {
+      int64_t* a = bins + ((int64_t)b * NV + v) * kXW + d;
+      t += __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  return t;
+}
+
 __device__ __forceinline__ float wave_sum_f32(float v) {
   v = xor_sum_f32<32>(v);
   v = xor_sum_f32<16>(v);
@@ -1090,7 +1213,13 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 3 : 1)) void gram_kernel(
     if (wi < n_work)
       gram_wave<NB, USER, true, BUF>(wi, work, idx, val, F, bias, k, ldk, zrow, direct, slab,
                                      cs, &scr[wid], drr, dpq, dqq, RHSM);
-    store_start_sums(drr, dpq, dqq, cs.parts);
+    if (cs.xbins) {   // one-pass CG: the entity's start sums, order-independent
+      const int lane = threadIdx.x & 63;
+      const int64_t t3[3] = {xterm(drr, lane), xterm(dpq, lane), xterm(dqq, lane)};
+      xsum_flush<3>(t3, cs.xbins);
+    } else {
+      store_start_sums(drr, dpq, dqq, cs.parts);
+    }
   }
 }
 
@@ -1106,7 +1235,13 @@ __global__ __launch_bounds__(256) void cg_start_split_kernel(const SplitItem* __
   double drr = 0.0, dpq = 0.0, dqq = 0.0;
   if (i < n_split)
     cg_start_entity<NB, USER>(split[i].entity, k, ldk, direct, cs, scr[wid], drr, dpq, dqq);
-  store_start_sums(drr, dpq, dqq, parts);
+  if (cs.xbins) {
+    const int lane = threadIdx.x & 63;
+    const int64_t t3[3] = {xterm(drr, lane), xterm(dpq, lane), xterm(dqq, lane)};
+    xsum_flush<3>(t3, cs.xbins);
+  } else {
+    store_start_sums(drr, dpq, dqq, parts);
+  }
 }
 
 template <int NB>
@@ -1698,6 +1833,63 @@ __device__ bool peer_sum(PeerComm* pc, double* vals, int count) {
   return true;
 }
 
+// The same exchange for the integer containers of the order-independent
+// sums, by a whole wave: lane l < count owns value l (it stores it into its
+// slot of every rank's record and sums the ranks' values for l); lane 0
+// advances the sequence number, tags after a system-scope release fence for
+// the wave's stores, and waits for the peers' tags (acquire).  Integer sums:
+// exact, so all ranks get the same containers.  Returns false on timeout
+// (every lane).
+__device__ bool peer_sum_lanes(PeerComm* pc, int64_t& val, int count) {
+  const int lane = threadIdx.x & 63;
+  uint32_t s = 0;
+  if (lane == 0) {
+    s = pc->seq + 1;
+    pc->seq = s;
+  }
+  s = __builtin_amdgcn_readfirstlane(s);
+  const int world = pc->world, rank = pc->rank;
+  const int64_t slot = s % kPeerSlots;
+  for (int q = 0; q < world; ++q) {
+    int64_t* rec = reinterpret_cast<int64_t*>(pc->buf[q]) + (slot * world + rank) * kPeerRec;
+    if (lane < count) __hip_atomic_store(rec + lane, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __threadfence_system();
+  if (lane == 0) {
+    for (int q = 0; q < world; ++q) {
+      int64_t* rec = reinterpret_cast<int64_t*>(pc->buf[q]) + (slot * world + rank) * kPeerRec;
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(rec + kPeerRec - 1), (uint64_t)s,
+                         __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  int ok = 1;
+  if (lane == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
+    for (int q = 0; q < world && ok; ++q) {
+      const int64_t* rec = reinterpret_cast<const int64_t*>(pc->buf[rank]) + (slot * world + q) * kPeerRec;
+      while (__hip_atomic_load(reinterpret_cast<const uint64_t*>(rec + kPeerRec - 1),
+                               __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != (uint64_t)s) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 3000000000ull) {
+          pc->error = 1;
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+  }
+  ok = __builtin_amdgcn_readfirstlane(ok);
+  if (!ok) return false;
+  __threadfence_system();
+  int64_t acc = 0;
+  for (int q = 0; q < world; ++q) {
+    const int64_t* rec = reinterpret_cast<const int64_t*>(pc->buf[rank]) + (slot * world + q) * kPeerRec;
+    if (lane < count) acc += __hip_atomic_load(rec + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (lane < count) val = acc;
+  return true;
+}
+
 // Self-test of a freshly mapped peer exchange: one reduction of
 // {rank + 1, 1}; out = {sum, count, ok}.  Run by every rank at attach time.
 __global__ void peer_selftest_kernel(PeerComm* pc, double* out) {
@@ -1707,6 +1899,34 @@ __global__ void peer_selftest_kernel(PeerComm* pc, double* out) {
   out[0] = v[0];
   out[1] = v[1];
   out[2] = ok ? 1.0 : 0.0;
+}
+
+// Test hook (mr_test_xsum): the order-independent sum of n terms dealt to
+// the waves of `gridDim.x` blocks (wave-strided), flushed into `bins`, then
+// collected and converted by one wave of a second launch.
+__global__ __launch_bounds__(256) void xsum_test_kernel(const double* __restrict__ t, int64_t n,
+                                                        int64_t* __restrict__ bins) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), W = (int64_t)gridDim.x * 4;
+  int64_t acc[1] = {0};
+  for (int64_t i = w; i < n; i += W) acc[0] += xterm(t[i], lane);
+  xsum_flush<1>(acc, bins);
+}
+__global__ void xsum_collect_kernel(int64_t* __restrict__ bins, double* __restrict__ out) {
+  __shared__ int64_t xs[kXW];
+  const int lane = threadIdx.x;
+  const int64_t c = xsum_collect<1>(bins, lane);
+  if (lane < kXW) xs[lane] = c;
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) out[0] = xsum_value(xs);
+}
+int launch_xsum_test(hipStream_t s, const double* t, int64_t n, int blocks, int64_t* bins,
+                     double* out) {
+  xsum_test_kernel<<<blocks, 256, 0, s>>>(t, n, bins);
+  MR_HIP(hipGetLastError());
+  xsum_collect_kernel<<<1, 64, 0, s>>>(bins, out);
+  MR_HIP(hipGetLastError());
+  return 0;
 }
 
 // Latency probe: `iters` back-to-back reductions of one value by one thread
@@ -2010,143 +2230,138 @@ void cg_onepass_kernel(
     const float* __restrict__ G, const float* __restrict__ Gs, const float* __restrict__ Gn,
     double* __restrict__ p, double* __restrict__ pb, double* __restrict__ r,
     double* __restrict__ rb, double* __restrict__ q, double* __restrict__ qb,
-    float* __restrict__ x, float* __restrict__ xb, double* __restrict__ partials,
+    float* __restrict__ x, float* __restrict__ xb, int64_t* __restrict__ xbins,
     CgMirror* mirror, int seq) {
   if (ald(&st->done)) return;
   const double beta = ald(&st->beta), alpha = ald(&st->alpha);
   constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2, NTILE = NO + NF + (NB & 1);
   constexpr int64_t GS = (int64_t)NTILE * 256 + NF * 16;   // == gsize_of(k)
   constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
+  constexpr int XC = xchunk_of(NB, USER);
   __shared__ MvScratch<NB> scr[MV_WAVES];
   __shared__ double rvs[MV_WAVES][16 * NB];
-  __shared__ double sh[MV_WAVES];
-  __shared__ double wacc[MV_WAVES][4];   // the wave's running p.q, r.q, q.q, r.r (off the VGPRs)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   MvScratch<NB>& sc = scr[wid];
   double* rs = rvs[wid];
-  if (lane < 4) wacc[wid][lane] = 0.0;
-  for (int64_t e = (int64_t)blockIdx.x * MV_WAVES + wid; e < E;
-       e += (int64_t)gridDim.x * MV_WAVES) {
-    double* pe = p + e * ldk;
-    double* re = r + e * ldk;
-    double* qe = q + e * ldk;
-    float* xe = x + e * ldk;
-    double pi[NV], ri[NV], qi[NV];
-    float xi[NV];
-#pragma unroll
-    for (int h = 0; h < NV; ++h) {
-      const int i = lane + 64 * h;
-      pi[h] = (i < NP) ? pe[i] : 0.0;
-      ri[h] = (i < NP) ? re[i] : 0.0;
-      qi[h] = (update && i < NP) ? qe[i] : 0.0;
-      xi[h] = (update && i < NP) ? xe[i] : 0.f;
-    }
-    double pbias = 0.0, rbias = 0.0, qbias = 0.0;
-    float xbias = 0.f;
-    double d = 0.0;   // r.r of the updated residual (matrix.cpp:507's direct dot)
-    if (USER) {
-      pbias = pb[e];
-      rbias = rb[e];
-      if (update) {
-        qbias = qb[e];
-        xbias = xb[e];
-      }
-    }
-    const floatx4* __restrict__ Ge = reinterpret_cast<const floatx4*>(G + e * GS);
-    float4 g[NTILE];
-#pragma unroll
-    for (int t = 0; t < NTILE; ++t) {
-      const floatx4 v4 = __builtin_nontemporal_load(Ge + t * 64 + lane);
-      g[t] = make_float4(v4[0], v4[1], v4[2], v4[3]);
-    }
-    float d2 = 0.f;
-    if (NF > 0 && lane < 16 * NF) d2 = G[e * GS + NTILE * 256 + lane];
-#pragma unroll
-    for (int h = 0; h < NV; ++h) {
-      const int i = lane + 64 * h;
-      if (i < NP) {
-        double rn = ri[h], pn = pi[h];
-        if (update) {
-          rn = fma(alpha, qi[h], ri[h]);
-          re[i] = rn;
-          xe[i] = (float)fma(alpha, pi[h], (double)xi[h]);
-          pn = fma(beta, pi[h], -rn);
-          pe[i] = pn;
-          d = fma(rn, rn, d);
-        }
-        sc.pv[virt_of(i, NB)] = pn;
-        rs[virt_of(i, NB)] = rn;
-      }
-    }
-    if (USER && update) {
-      const double rbn = fma(alpha, qbias, rbias);
-      const double pbn = fma(beta, pbias, -rbn);
-      if (lane == 0) {
-        rb[e] = rbn;
-        xb[e] = (float)fma(alpha, pbias, (double)xbias);
-        pb[e] = pbn;
-      }
-      rbias = rbn;
-      pbias = pbn;
-      if (lane == 0) d = fma(rbn, rbn, d);
-    }
-    if (NF > 0 && lane < 16 * NF) sc.dd[lane] = d2;
-    __builtin_amdgcn_wave_barrier();
-    double yo[NV], ybv = 0.0;
-    tile_matvec<NB, USER, (NB > 4) || MR_OP_OPAQUE>(g, sc, pbias, USER ? Gs + e * ldk : nullptr,
-                                                    USER ? Gn[e] : 0.f, k, yo,
-                          ybv);
+  // the wave's p.q, r.q, q.q, r.r as order-independent sums (lane = digit),
+  // one term per chunk of XC consecutive entities: the chunk's partial sums
+  // run lane-wise in entity order and are reduced across the wave once, so a
+  // term depends only on its chunk, never on the grid
+  // (the block's containers live in LDS, added to by LDS integer atomics:
+  // no registers held across the GEMV)
+  __shared__ int64_t xacc[1][4][kXW];
+  if (threadIdx.x < 4 * kXW) (&xacc[0][0][0])[threadIdx.x] = 0;
+  __syncthreads();
+  const int wu = __builtin_amdgcn_readfirstlane(wid);   // wave-uniform: scalar loop state
+  for (int64_t c0 = ((int64_t)blockIdx.x * MV_WAVES + wu) * XC; c0 < E;
+       c0 += (int64_t)gridDim.x * MV_WAVES * XC) {
+    const int64_t c1 = c0 + XC < E ? c0 + XC : E;
     double a = 0.0, b = 0.0, c = 0.0;
+    double d = 0.0;   // r.r of the updated residual (matrix.cpp:507's direct dot)
+    for (int64_t e = c0; e < c1; ++e) {
+      double* pe = p + e * ldk;
+      double* re = r + e * ldk;
+      double* qe = q + e * ldk;
+      float* xe = x + e * ldk;
+      double pi[NV], ri[NV], qi[NV];
+      float xi[NV];
 #pragma unroll
-    for (int h = 0; h < NV; ++h) {
-      const int o = lane + 64 * h;
-      if (o < NP) {
-        const int n = nat_of(o, NB);
-        if (n < k) {
-          qe[n] = yo[h];
-          a = fma(yo[h], sc.pv[o], a);
-          b = fma(yo[h], rs[o], b);
-          c = fma(yo[h], yo[h], c);
+      for (int h = 0; h < NV; ++h) {
+        const int i = lane + 64 * h;
+        pi[h] = (i < NP) ? pe[i] : 0.0;
+        ri[h] = (i < NP) ? re[i] : 0.0;
+        qi[h] = (update && i < NP) ? qe[i] : 0.0;
+        xi[h] = (update && i < NP) ? xe[i] : 0.f;
+      }
+      double pbias = 0.0, rbias = 0.0, qbias = 0.0;
+      float xbias = 0.f;
+      if (USER) {
+        pbias = pb[e];
+        rbias = rb[e];
+        if (update) {
+          qbias = qb[e];
+          xbias = xb[e];
         }
       }
-    }
-    if (USER && lane == 0) {
-      qb[e] = ybv;
-      a = fma(ybv, pbias, a);
-      b = fma(ybv, rbias, b);
-      c = fma(ybv, ybv, c);
+      const floatx4* __restrict__ Ge = reinterpret_cast<const floatx4*>(G + e * GS);
+      float4 g[NTILE];
+#pragma unroll
+      for (int t = 0; t < NTILE; ++t) {
+        const floatx4 v4 = __builtin_nontemporal_load(Ge + t * 64 + lane);
+        g[t] = make_float4(v4[0], v4[1], v4[2], v4[3]);
+      }
+      float d2 = 0.f;
+      if (NF > 0 && lane < 16 * NF) d2 = G[e * GS + NTILE * 256 + lane];
+#pragma unroll
+      for (int h = 0; h < NV; ++h) {
+        const int i = lane + 64 * h;
+        if (i < NP) {
+          double rn = ri[h], pn = pi[h];
+          if (update) {
+            rn = fma(alpha, qi[h], ri[h]);
+            re[i] = rn;
+            xe[i] = (float)fma(alpha, pi[h], (double)xi[h]);
+            pn = fma(beta, pi[h], -rn);
+            pe[i] = pn;
+            d = fma(rn, rn, d);
+          }
+          sc.pv[virt_of(i, NB)] = pn;
+          rs[virt_of(i, NB)] = rn;
+        }
+      }
+      if (USER && update) {
+        const double rbn = fma(alpha, qbias, rbias);
+        const double pbn = fma(beta, pbias, -rbn);
+        if (lane == 0) {
+          rb[e] = rbn;
+          xb[e] = (float)fma(alpha, pbias, (double)xbias);
+          pb[e] = pbn;
+        }
+        rbias = rbn;
+        pbias = pbn;
+        if (lane == 0) d = fma(rbn, rbn, d);
+      }
+      if (NF > 0 && lane < 16 * NF) sc.dd[lane] = d2;
+      __builtin_amdgcn_wave_barrier();
+      double yo[NV], ybv = 0.0;
+      tile_matvec<NB, USER, (NB > 4) || MR_OP_OPAQUE>(g, sc, pbias, USER ? Gs + e * ldk : nullptr,
+                                                      USER ? Gn[e] : 0.f, k, yo, ybv);
+#pragma unroll
+      for (int h = 0; h < NV; ++h) {
+        const int o = lane + 64 * h;
+        if (o < NP) {
+          const int n = nat_of(o, NB);
+          if (n < k) {
+            qe[n] = yo[h];
+            a = fma(yo[h], sc.pv[o], a);
+            b = fma(yo[h], rs[o], b);
+            c = fma(yo[h], yo[h], c);
+          }
+        }
+      }
+      if (USER && lane == 0) {
+        qb[e] = ybv;
+        a = fma(ybv, pbias, a);
+        b = fma(ybv, rbias, b);
+        c = fma(ybv, ybv, c);
+      }
+      __builtin_amdgcn_wave_barrier();
     }
     a = wave_sum_f64(a);
     b = wave_sum_f64(b);
     c = wave_sum_f64(c);
     d = wave_sum_f64(d);
-    if (lane == 0) {
-      wacc[wid][0] += a;
-      wacc[wid][1] += b;
-      wacc[wid][2] += c;
-      wacc[wid][3] += d;
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-  const int64_t np = gridDim.x;
-  double tot[4];
-  __syncthreads();
-  if (threadIdx.x == 0) {   // waves in order, as block_sum_f64 sums them
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      double t = 0.0;
-      for (int w = 0; w < MV_WAVES; ++w) t += wacc[w][j];
-      tot[j] = t;
+    if (lane < kXW) {
+      atomicAdd((unsigned long long*)&xacc[0][0][lane], (unsigned long long)xterm(a, lane));
+      atomicAdd((unsigned long long*)&xacc[0][1][lane], (unsigned long long)xterm(b, lane));
+      atomicAdd((unsigned long long*)&xacc[0][2][lane], (unsigned long long)xterm(c, lane));
+      atomicAdd((unsigned long long*)&xacc[0][3][lane], (unsigned long long)xterm(d, lane));
     }
   }
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      __hip_atomic_store(&partials[j * np + blockIdx.x], tot[j], __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-  }
+  xsum_flush_lds<4>(xacc, xbins, 1);
   // last-arriving block: iteration t's scalars (see last_block_finalize for
-  // the memory-model basis of this hand-off)
+  // the memory-model basis of this hand-off; the bins' atomics are drained
+  // by the same vmcnt wait as a partial store)
   __shared__ int s_last;
   if (threadIdx.x == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2154,24 +2369,22 @@ void cg_onepass_kernel(
                                     __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   }
   __syncthreads();
-  if (!s_last) return;
-  double sum[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    double acc = 0.0;
-    for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x)
-      acc += __hip_atomic_load(&partials[j * np + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sum[j] = block_sum_f64<256>(acc, sh);
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    __hip_atomic_store(&st->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (PeerComm* pc = ald(&st->peer)) {
-      if (!peer_sum(pc, sum, 4)) {
-        peer_fail(st, mirror, seq);
-        return;
-      }
+  if (!s_last || wid != 0) return;
+  __shared__ int64_t xs[4 * kXW];
+  int64_t tot = xsum_collect<4>(xbins, lane);
+  if (lane == 0) __hip_atomic_store(&st->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (PeerComm* pc = ald(&st->peer)) {
+    if (!peer_sum_lanes(pc, tot, 4 * kXW)) {
+      if (lane == 0) peer_fail(st, mirror, seq);
+      return;
     }
+  }
+  if (lane < 4 * kXW) xs[lane] = tot;
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) {
+    double sum[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sum[j] = xsum_value(&xs[j * kXW]);
     CgScalars v = load_state(st);
     // iteration t >= 1: alpha and the next r'.r' start from the DIRECT r.r of
     // the residual just updated, not from the previous kernel's derived value,
@@ -2208,16 +2421,16 @@ int onepass_blocks_per_cu(bool user_side, int k) {
 int launch_cg_onepass(hipStream_t s, bool user_side, CgState* st, int update, int64_t E, int k,
                       const float* G, const float* Gs, const float* Gn, double* p, double* pb,
                       double* r, double* rb, double* q, double* qb, float* x, float* xb,
-                      double* partials, int n_part, CgMirror* mirror, int seq) {
+                      int64_t* xbins, int n_part, CgMirror* mirror, int seq) {
   if (n_part <= 0) return 0;
 #define MR_OP_CASE(NB)                                                                      \
   case NB:                                                                                  \
     if (user_side)                                                                          \
       MR_LAUNCH((cg_onepass_kernel<NB, true>), dim3(n_part), dim3(256), 0, s, st, update, E, \
-                k, ldk_of(k), G, Gs, Gn, p, pb, r, rb, q, qb, x, xb, partials, mirror, seq); \
+                k, ldk_of(k), G, Gs, Gn, p, pb, r, rb, q, qb, x, xb, xbins, mirror, seq);    \
     else                                                                                    \
       MR_LAUNCH((cg_onepass_kernel<NB, false>), dim3(n_part), dim3(256), 0, s, st, update,  \
-                E, k, ldk_of(k), G, Gs, Gn, p, pb, r, rb, q, qb, x, xb, partials, mirror,  \
+                E, k, ldk_of(k), G, Gs, Gn, p, pb, r, rb, q, qb, x, xb, xbins, mirror,     \
                 seq);                                                                       \
     break;
   switch (nb16_of(k)) {
@@ -2551,11 +2764,34 @@ constexpr int CTL_THREADS = 1024;
 __global__ __launch_bounds__(CTL_THREADS) void cg_control_kernel(
     CgState* __restrict__ st, int phase, int ctl,
     const double* __restrict__ partials, int n_part, CgMirror* mirror, int seq,
-    double min_dec, int max_it, int sharded) {
+    double min_dec, int max_it, int sharded, int64_t* __restrict__ start_xbins) {
   if (phase != CG_INIT && phase != CG_START && ald(&st->done)) return;
   __shared__ double sh[CTL_THREADS / 64];
   if (ctl & CTL_REDUCE) {
-    if (phase == CG_START) {
+    if (phase == CG_START && start_xbins) {
+      // one-pass CG: the start's sums from the order-independent bins (wave
+      // 0), exchanged as integers with the peers, then to fp64
+      if (threadIdx.x >= 64) return;
+      const int lane = threadIdx.x;
+      __shared__ int64_t xs[3 * kXW];
+      int64_t t = xsum_collect<3>(start_xbins, lane);
+      PeerComm* pc = ald(&st->peer);
+      if (pc && (ctl & CTL_FINALIZE) && !peer_sum_lanes(pc, t, 3 * kXW)) {
+        if (lane == 0) {
+          ast(&st->comm[0], 0.0);
+          ast(&st->comm[1], 0.0);
+          peer_fail(st, mirror, seq);
+        }
+        return;
+      }
+      if (lane < 3 * kXW) xs[lane] = t;
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) {
+        ast(&st->comm[0], xsum_value(&xs[0]));
+        ast(&st->comm[1], xsum_value(&xs[kXW]));
+        ast(&st->comm[2], xsum_value(&xs[2 * kXW]));
+      }
+    } else if (phase == CG_START) {
       // (r.r, p.Gp, q.q) triples (one per Gram block: ~E/4 of them, written
       // by every XCD): thread t sums triples t, t + T, t + 2T, ... in order,
       // 8 loads in flight, then the fixed-order block tree.
@@ -2647,9 +2883,9 @@ __global__ __launch_bounds__(CTL_THREADS) void cg_control_kernel(
 
 int launch_cg_control(hipStream_t s, CgState* st, int phase, int ctl,
                       const double* partials, int n_part, CgMirror* mirror, int seq,
-                      double min_dec, int max_it, int sharded) {
+                      double min_dec, int max_it, int sharded, int64_t* start_xbins) {
   MR_LAUNCH(cg_control_kernel, dim3(1), dim3(CTL_THREADS), 0, s, st, phase, ctl, partials, n_part,
-                                                  mirror, seq, min_dec, max_it, sharded);
+                                                  mirror, seq, min_dec, max_it, sharded, start_xbins);
   MR_HIP(hipGetLastError());
   return 0;
 }

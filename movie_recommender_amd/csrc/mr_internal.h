@@ -170,17 +170,21 @@ struct CgStart {
   const float* xb;   // user side: bias column of the iterate
   double *r, *rb, *p, *pb, *q, *qb;   // fp64 CG vectors
   double* parts;
+  // one-pass CG: the start's (r.r, p.Gp, q.q) as order-independent sums in
+  // these kXBins x 3 x 11 int64 bins instead of per-block parts (nullptr:
+  // the parts); read and reset by the CG_START control
+  int64_t* xbins;
 };
 
 // Peer all-reduce of the CG scalars over IPC-mapped device memory (sharded
 // runs; Engine::set_peer).  Every rank owns an exchange buffer of
-// kPeerSlots x world records {v0 .. v6, tag} in uncached device memory and
+// kPeerSlots x world records {v0 .. v62, tag} in uncached device memory and
 // maps every peer's.  Reduction s writes this rank's values into record
 // (s % kPeerSlots, rank) of EVERY rank's buffer, then the tag s (release,
 // system scope); each rank then waits for the tag of every record of its own
 // buffer and sums the values in rank order -- so all ranks get the same bits.
 constexpr int kPeerSlots = 16;
-constexpr int kPeerRec = 8;    // doubles per record: up to 7 values, then the tag
+constexpr int kPeerRec = 64;   // 8-byte words per record: up to 63 values, then the tag
 constexpr int kMaxPeers = 64;
 struct PeerComm {
   int32_t world, rank;
@@ -191,6 +195,10 @@ struct PeerComm {
 
 // One peer reduction of {rank + 1, 1} into out[0..2] = {sum, count, ok}.
 int launch_peer_selftest(hipStream_t s, PeerComm* pc, double* out);
+// Test hook: the order-independent sum (kernels.hip xterm / xsum_value) of
+// n terms over `blocks` blocks; bins: 16 x 1 x 11 int64 zeros (left zero).
+int launch_xsum_test(hipStream_t s, const double* t, int64_t n, int blocks, int64_t* bins,
+                     double* out);
 // `iters` reductions of one value back to back; out = {ok, iters done}.
 int launch_peer_bench(hipStream_t s, PeerComm* pc, int iters, double* out);
 
@@ -280,8 +288,12 @@ int onepass_blocks_per_cu(bool user_side, int k);
 int launch_cg_onepass(hipStream_t s, bool user_side, CgState* st, int update, int64_t E, int k,
                       const float* G, const float* Gs, const float* Gn, double* p, double* pb,
                       double* r, double* rb, double* q, double* qb, float* x, float* xb,
-                      double* partials, int n_part, CgMirror* mirror, int seq);
-// x is the fp32 factor table (and bias), r / p / q the fp64 CG vectors.
+                      int64_t* xbins, int n_part, CgMirror* mirror, int seq);
+// x is the fp32 factor table (and bias), r / p / q the fp64 CG vectors;
+// xbins: kXBins x 4 x 11 int64 bins of the order-independent sums (zero
+// between launches: the last block reads and resets them).
+constexpr int kXBinWords = 16 * 4 * 11;       // kXBins x sums x (kXD + 1), kernels.hip
+constexpr int kXBinStartWords = 16 * 3 * 11;  // the fused start's three sums
 // mode UPD_FINISH: apply a one-pass solve's pending last update (no sums).
 int launch_cg_update(hipStream_t s, const CgState* st, int mode, int64_t n,
                      int64_t nb, float* x, double* r, double* p, const double* q,
@@ -296,7 +308,8 @@ int launch_x_to_vec(hipStream_t s, int64_t n, int64_t nb, const float* x, const 
 // sharded initialise the state.
 int launch_cg_control(hipStream_t s, CgState* st, int phase, int ctl,
                       const double* partials, int n_part, CgMirror* mirror = nullptr,
-                      int seq = 0, double min_dec = 0.0, int max_it = 0, int sharded = 0);
+                      int seq = 0, double min_dec = 0.0, int max_it = 0, int sharded = 0,
+                      int64_t* start_xbins = nullptr);
 int launch_solve(hipStream_t s, bool user_side, int64_t E, int k, double ridge,
                  const float* G, const float* Gs, const float* Gn,
                  const float* C, const float* Cb, float* x, float* xb,

@@ -25,15 +25,23 @@ import numpy as np
 from . import _lib
 
 
-def shard_bounds(counts, world):
-    """Contiguous id ranges with ~equal rating counts: ``world+1`` boundaries."""
+# entities per term of the one-pass CG's order-independent sums (kernels.hip
+# kXChunk): interior shard boundaries at multiples of it give every rank the
+# single-GPU run's terms, so a sharded run reproduces its scalars bit for bit
+SUM_CHUNK = 4
+
+
+def shard_bounds(counts, world, align=SUM_CHUNK):
+    """Contiguous id ranges with ~equal rating counts: ``world+1`` boundaries,
+    the interior ones rounded to the nearest multiple of ``align``."""
     counts = np.asarray(counts, np.int64)
     n = len(counts)
     csum = np.concatenate([[0], np.cumsum(counts)])
     total = csum[-1]
     b = [0]
     for r in range(1, world):
-        b.append(int(np.searchsorted(csum, total * r / world, side="left")))
+        c = int(np.searchsorted(csum, total * r / world, side="left"))
+        b.append(int(round(c / align)) * align)
     b.append(n)
     b = np.maximum.accumulate(np.minimum(np.array(b, np.int64), n))
     return b

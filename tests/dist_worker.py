@@ -82,11 +82,13 @@ def oracle_sharded(d, max_iteration, rank, world):
     return U, V, it
 
 
-def skewed_bounds(n, world):
+def skewed_bounds(n, world, align=1):
     """Deliberately uneven shards (rank r's share grows as 2^r): the padded
-    exchange then carries mostly padding for the small ranks."""
+    exchange then carries mostly padding for the small ranks.  ``align``
+    rounds the interior boundaries down to its multiples."""
     w = 2.0 ** np.arange(world)
-    b = np.concatenate([[0], np.floor(np.cumsum(w) / w.sum() * n)]).astype(np.int64)
+    b = np.concatenate([[0], np.floor(np.cumsum(w) / w.sum() * n / align) * align])
+    b = b.astype(np.int64)
     b[-1] = n
     return b
 
@@ -99,7 +101,11 @@ def engine_sharded(d, max_iteration, rank, world, mode, skew=False, onepass=1):
     dev = rank % max(1, device_count())
     comm = "rccl" if mode == "engine_rccl" else TorchComm()
     nU, nI = int(d["num_users"]), int(d["num_items"])
-    bounds = (skewed_bounds(nU, world), skewed_bounds(nI, world)) if skew else None
+    # peer runs: boundaries at the sums' chunk size (distributed.SUM_CHUNK),
+    # which the bitwise sharded == single-GPU test needs; gloo runs keep
+    # arbitrary ones
+    al = 4 if mode == "engine_peer" else 1
+    bounds = (skewed_bounds(nU, world, al), skewed_bounds(nI, world, al)) if skew else None
     ctx = sharded_context(d["user_ids"], d["item_ids"], d["ratings"], k, nU, nI, dev, comm,
                           bounds=bounds, scalars="peer" if mode == "engine_peer" else "collective")
     if mode == "engine_peer" and not ctx.peer_scalars:

@@ -54,7 +54,7 @@ def test_entity_cost_balances_gram_and_cg_work():
     """Light entities cost a CG pass each: with the per-entity term the
     rank holding many light users gets fewer of them than a pure rating
     balance would give it."""
-    from movie_recommender_amd.distributed import entity_cost, shard_bounds
+    from movie_recommender_amd.distributed import SUM_CHUNK, entity_cost, shard_bounds
     counts = np.concatenate([np.full(1000, 500), np.full(20000, 25)])   # heavy then light
     plain = shard_bounds(counts, 2)
     cost = entity_cost(counts, 64)
@@ -62,7 +62,9 @@ def test_entity_cost_balances_gram_and_cg_work():
     b = shard_bounds(cost, 2)
     assert b[1] > plain[1]                 # the heavy rank takes some light users
     load = [cost[b[r]:b[r + 1]].sum() for r in range(2)]
-    assert abs(load[0] - load[1]) <= cost.max()
+    # one entity of imbalance, plus the rounding to a multiple of SUM_CHUNK
+    # (up to SUM_CHUNK / 2 entities moved, each load by as many)
+    assert abs(load[0] - load[1]) <= (SUM_CHUNK + 1) * cost.max()
 
 
 def test_shard_views_partition_every_rating():
@@ -130,6 +132,17 @@ def test_callback_transport_padded_exchange_gloo_cpu(tmp_path):
         assert np.array_equal(blk, 1000 * r + np.arange(maxrows * ldk, dtype=np.float32))
         assert np.array_equal(tab_b[r * maxrows:(r + 1) * maxrows],
                               1000 * r + np.arange(maxrows, dtype=np.float32) + 0.5)
+
+
+def test_shard_bounds_aligned_to_sum_chunk():
+    """Interior boundaries at multiples of the one-pass CG's sum chunk (the
+    condition for sharded == single-GPU bit for bit)."""
+    from movie_recommender_amd.distributed import SUM_CHUNK, shard_bounds
+    rng = np.random.default_rng(3)
+    for n, world in ((103, 2), (1000, 3), (50367, 8), (9, 4)):
+        b = shard_bounds(rng.integers(1, 500, n), world)
+        assert b[0] == 0 and b[-1] == n and np.all(np.diff(b) >= 0)
+        assert all(int(x) % SUM_CHUNK == 0 or int(x) == n for x in b[1:-1])
 
 
 def test_skewed_bounds_cover_and_grow():
@@ -299,3 +312,16 @@ def test_engine_peer_scalars_match_collective(gpu, tmp_path, fixture, max_it, np
                                onepass=1)
     assert ret1 == int(d["ret"])
     assert rel_err(U1, d["U"]) < 1e-5 and rel_err(V1, d["V"]) < 1e-5
+    if int(d["k"]) <= 64:
+        # one-pass CG with its fused start: every cross-entity sum is an exact
+        # integer sum (kernels.hip "Order-independent CG sums"), so the
+        # sharded run reproduces the single-GPU run bit for bit
+        from movie_recommender_amd.engine import AlsContext
+        with AlsContext(d["user_ids"], d["item_ids"], d["ratings"], int(d["k"]),
+                        int(d["num_users"]), int(d["num_items"])) as ctx:
+            ctx.set_option("cg_onepass", 1)
+            ctx.set_factors(d["U0"], d["V0"])
+            ret_s = ctx.run(0.01, max_it)
+            Us, Vs = ctx.get_factors()
+        assert ret_s == ret1
+        assert np.array_equal(Us, U1) and np.array_equal(Vs, V1), (rel_err(U1, Us), rel_err(V1, Vs))

@@ -138,3 +138,37 @@ def test_cg_rejects_bad_input(gpu):
     ci = np.array([0, 1, 1], np.int32)
     assert not L.mr_cg_create(0, 2, 3, rp.ctypes.data_as(_lib.IP), ci.ctypes.data_as(_lib.IP),
                               v.ctypes.data_as(_lib.DP))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("blocks", [1, 3, 64])
+def test_xsum_device_is_order_independent_and_matches_restatement(gpu, blocks):
+    """The one-pass CG's order-independent sums on the device (mr_test_xsum:
+    terms dealt to the waves of `blocks` blocks, flushed into the bins with
+    integer atomics, collected by one wave) equal the restatement
+    (oracle/xsum.py) bit for bit, for any order of the terms and any number
+    of blocks -- the property that makes sharded runs reproduce the
+    single-GPU scalars."""
+    import ctypes
+    import math
+    from movie_recommender_amd import _lib
+    from oracle import xsum as X
+    rng = np.random.default_rng(blocks)
+    cases = [rng.normal(0, 1, 10000),
+             rng.normal(0, 1e12, 3000) * rng.uniform(0.5, 2, 3000) ** 8,
+             np.concatenate([rng.normal(0, 1e-40, 100), [1e20, -1e20, 5e-324, -0.0, 0.0]]),
+             rng.uniform(-1, 1, 777) * 2.0 ** 94,
+             np.array([1.0, np.inf, 2.0]), np.array([2.0 ** 96]), np.zeros(0)]
+    L = _lib.lib()
+    for t in cases:
+        want = X.xsum(t)
+        for order in (t, t[::-1], rng.permutation(t)):
+            o = np.ascontiguousarray(order, np.float64)
+            out = ctypes.c_double(0.0)
+            _lib.check(L.mr_test_xsum(0, o.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                      len(o), blocks, ctypes.byref(out)), "mr_test_xsum")
+            if math.isnan(want):
+                assert math.isnan(out.value)
+            else:
+                assert np.float64(out.value).view(np.int64) == np.float64(want).view(np.int64), \
+                    (out.value, want)

@@ -195,3 +195,26 @@ def test_scipy_path_restatement_solves_the_design_matrix():
         B[t, i[t] * k:(i[t] + 1) * k] = x.reshape(-1, k + 1)[u[t], :k]
     ref2 = np.linalg.lstsq(B, r - x[3::4][u], rcond=None)[0]
     assert np.max(np.abs(y - ref2)) < 1e-6
+
+
+def test_xsum_restatement_is_the_exact_sum():
+    """CPU: oracle/xsum (the engine's order-independent CG sums) equals the
+    exactly rounded sum of the truncated terms to within one ulp, and does
+    not depend on the terms' order."""
+    import math
+    from fractions import Fraction
+    import numpy as np
+    from oracle import xsum as X
+    rng = np.random.default_rng(5)
+    for scale in (1e-30, 1e-3, 1.0, 1e7, 1e20):
+        t = rng.normal(0, scale, 5000) * rng.uniform(0.5, 2.0, 5000) ** 10
+        a = X.xsum(t)
+        b = X.xsum(t[::-1])
+        c = X.xsum(rng.permutation(t))
+        assert a == b == c
+        exact = sum((Fraction(int(Fraction(abs(x)) * 2 ** 192)) * (1 if x >= 0 else -1)
+                     for x in t), Fraction(0)) / 2 ** 192
+        assert abs(Fraction(a) - exact) <= Fraction(abs(a)) * 2 ** -51 + Fraction(2) ** -190
+    assert math.isnan(X.xsum([1.0, float("inf")]))
+    assert math.isnan(X.xsum([2.0 ** 97]))
+    assert X.xsum([]) == 0.0 and X.xsum([0.0, -0.0]) == 0.0

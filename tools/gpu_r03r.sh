@@ -1,0 +1,33 @@
+#!/bin/bash
+# round 3 session r: chunked order-independent CG sums -- the xsum / parity /
+# distributed GPU tests, smoke, fixed-count A/B against the committed build,
+# default bench.
+set -o pipefail
+OUT=gpurun_out/r03r; mkdir -p $OUT
+export TMPDIR=/tmp
+step() {  # name, seconds, command...
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 $secs "$@"
+  local rc=$?
+  if [ $rc -ne 0 ]; then echo "$name rc=$rc: stop"; exit $rc; fi
+}
+timeout -k 10 700 python -u -m pytest tests/test_gpu_cgls.py tests/test_gpu_parity.py tests/test_distributed.py -m gpu -v --timeout 400 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+rc=$?; grep -E "FAILED|ERROR|passed|failed" $OUT/gpu_tests.log | tail -12
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "TESTS rc=$rc: stop"; exit $rc; fi
+step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+tail -1 $OUT/smoke.log
+for k in 64 128; do
+  step ab_new_$k 300 python -u tools/cg_ab.py --k $k --tag new > $OUT/ab_new_k$k.json 2> $OUT/ab_new_k$k.err
+  MR_LIB_PATH=var_libs/head/cpp_ls_lib.so step ab_head_$k 300 python -u tools/cg_ab.py --k $k --tag head > $OUT/ab_head_k$k.json 2> $OUT/ab_head_k$k.err
+done
+python3 - <<'PY'
+import json
+for k in (64, 128):
+    for t in ("new", "head"):
+        d = json.load(open(f"gpurun_out/r03r/ab_{t}_k{k}.json"))
+        print(k, t, "users", d["users"]["ms_per_cg_iteration"], d["users"]["kernels"].get("matvec_users"),
+              "items", d["items"]["ms_per_cg_iteration"], d["items"]["kernels"].get("matvec_items"))
+PY
+step bench 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err
+cut -c1-300 $OUT/bench.json
+echo DONE
