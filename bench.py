@@ -247,6 +247,8 @@ def main():
                     help="time steps without per-launch HIP events (no roofline)")
     ap.add_argument("--cg-speculate", type=int, default=None,
                     help="engine launch-ahead level (include/mr_als.h MR_OPT_CG_SPECULATE)")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="engine option NAME=VALUE (engine.OPTIONS), repeatable")
     ap.add_argument("--cpu-scale", type=float, default=0.25)
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="reference threads (default: this process's CPU share)")
@@ -331,6 +333,9 @@ def main():
         ctx.set_option("cg_onepass", 0)
     if args.cg_speculate is not None:
         ctx.set_option("cg_speculate", args.cg_speculate)
+    for o in args.opt:
+        name, val = o.split("=")
+        ctx.set_option(name, float(val))
     ctx.sync()
     log(f"[bench] context built in {time.perf_counter() - t0:.2f} s")
 

@@ -174,9 +174,16 @@ int mr_als_set_timing(mr_als* ctx, int enable);
  *                         every user-view rating is exact in bf16 (half-star
  *                         ratings, rating - median: always; measured -4 % at
  *                         k = 128, level at k = 64, where the VALU path
- *                         stays); 0: always on the VALU (fp32, rating order) */
+ *                         stays); 0: always on the VALU (fp32, rating order)
+ *   MR_OPT_CG_SWEEP       sweep direction of the one-pass CG kernel over the
+ *                         entity chunks: 1 (default) alternates, the first
+ *                         iteration after the start backwards (it starts on
+ *                         the lines the previous pass left in the Infinity
+ *                         Cache); 2 alternates the other way; 0 always
+ *                         forwards.  Results are identical in every mode (each
+ *                         chunk's partial sums are order-independent terms) */
 enum { MR_OPT_FUSE_START = 0, MR_OPT_CG_SPECULATE = 1, MR_OPT_WAIT_TIMEOUT_S = 2,
-       MR_OPT_CG_ONEPASS = 3, MR_OPT_GRAM_RHS_MFMA = 4 };
+       MR_OPT_CG_ONEPASS = 3, MR_OPT_GRAM_RHS_MFMA = 4, MR_OPT_CG_SWEEP = 5 };
 int mr_als_set_option(mr_als* ctx, int option, double value);
 /* Ratings per Gram work item: heavier entities are split across waves and
  * their partial normal equations combined in order.  Applies to contexts

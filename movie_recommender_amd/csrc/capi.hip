@@ -284,6 +284,10 @@ int mr_als_set_option(mr_als* ctx, int option, double value) {
     case MR_OPT_FUSE_START: ctx->eng.fuse_start = value != 0.0; return 0;
     case MR_OPT_CG_ONEPASS: ctx->eng.onepass = value != 0.0; return 0;
     case MR_OPT_GRAM_RHS_MFMA: ctx->eng.rhs_mfma = value != 0.0; return 0;
+    case MR_OPT_CG_SWEEP:
+      MR_CHECK(value == 0.0 || value == 1.0 || value == 2.0, "cg_sweep must be 0, 1 or 2");
+      ctx->eng.sweep = (int)value;
+      return 0;
     case MR_OPT_CG_SPECULATE:
       // every rank of a sharded run must use the same level (it decides which
       // launches, and with them which collectives, are issued)

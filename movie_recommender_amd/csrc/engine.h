@@ -84,6 +84,7 @@ struct Engine {
   bool fuse_start = true;   // CG start in the Gram epilogue (MR_OPT_FUSE_START)
   bool onepass = true;      // one kernel per CG iteration (MR_OPT_CG_ONEPASS)
   bool rhs_mfma = true;     // user-side rhs on the matrix cores (MR_OPT_GRAM_RHS_MFMA)
+  int sweep = 1;            // one-pass sweep direction per iteration (MR_OPT_CG_SWEEP)
   bool w_bf16 = false;      // every user-view rating is exact in bf16 (set by init)
   int speculate = 1;        // 0: never enqueue ahead; 1: enqueue t+2 while t+1 runs when
                             // state t proves t+1 cannot stop; 2: always one ahead

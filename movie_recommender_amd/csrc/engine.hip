@@ -1109,7 +1109,10 @@ int Engine::cg_onepass(Side& S, double min_dec, int max_it, double* final_rr, bo
     seq_of.push_back(++mirror_seq);
     hipEvent_t ev = nullptr;
     if (tic(mv_cls, t, &ev)) return -1;
-    if (launch_cg_onepass(stream, user, d_state, t > 0 ? 1 : 0, S.E, k, S.G, S.Gs, S.Gn, S.p,
+    // sweep 1: iteration 1 (the first kernel behind a fused start) runs
+    // backwards over the entities the Gram just wrote, then alternate
+    const int rev = sweep == 0 ? 0 : ((t & 1) ^ (sweep == 2 ? 1 : 0));
+    if (launch_cg_onepass(stream, user, d_state, t > 0 ? 1 : 0, rev, S.E, k, S.G, S.Gs, S.Gn, S.p,
                           S.pb, S.r, S.rb, S.q, S.qb, xf, xb, xbins, S.n_part_op, d_mirror,
                           seq_of.back()))
       return -1;

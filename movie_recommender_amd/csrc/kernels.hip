@@ -2220,13 +2220,16 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 4 : 2)) void cg_matvec_kernel(
 #ifndef MR_OP_WAVES
 #define MR_OP_WAVES 4
 #endif
+#ifndef MR_OP_GNT   // non-temporal G tile loads in the one-pass kernel
+#define MR_OP_GNT 1
+#endif
 template <int NB, bool USER>
 __global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 : MR_OP_WAVES) : 2))
 #ifdef MR_OP_WPE
 __attribute__((amdgpu_waves_per_eu(MR_OP_WPE, MR_OP_WPE)))
 #endif
 void cg_onepass_kernel(
-    CgState* __restrict__ st, int update, int64_t E, int k, int ldk,
+    CgState* __restrict__ st, int update, int rev, int64_t E, int k, int ldk,
     const float* __restrict__ G, const float* __restrict__ Gs, const float* __restrict__ Gn,
     double* __restrict__ p, double* __restrict__ pb, double* __restrict__ r,
     double* __restrict__ rb, double* __restrict__ q, double* __restrict__ qb,
@@ -2253,8 +2256,14 @@ void cg_onepass_kernel(
   if (threadIdx.x < 4 * kXW) (&xacc[0][0][0])[threadIdx.x] = 0;
   __syncthreads();
   const int wu = __builtin_amdgcn_readfirstlane(wid);   // wave-uniform: scalar loop state
-  for (int64_t c0 = ((int64_t)blockIdx.x * MV_WAVES + wu) * XC; c0 < E;
-       c0 += (int64_t)gridDim.x * MV_WAVES * XC) {
+  // rev: the grid sweeps the chunks from the last to the first (entity order
+  // inside a chunk unchanged, so every chunk's term is the same): alternate
+  // iterations then start where the previous sweep ended, on the lines it
+  // left in the Infinity Cache (DESIGN.md "Sweep direction")
+  const int64_t nch = (E + XC - 1) / XC;
+  for (int64_t j = (int64_t)blockIdx.x * MV_WAVES + wu; j < nch;
+       j += (int64_t)gridDim.x * MV_WAVES) {
+    const int64_t c0 = (rev ? nch - 1 - j : j) * XC;
     const int64_t c1 = c0 + XC < E ? c0 + XC : E;
     double a = 0.0, b = 0.0, c = 0.0;
     double d = 0.0;   // r.r of the updated residual (matrix.cpp:507's direct dot)
@@ -2287,7 +2296,7 @@ void cg_onepass_kernel(
       float4 g[NTILE];
 #pragma unroll
       for (int t = 0; t < NTILE; ++t) {
-        const floatx4 v4 = __builtin_nontemporal_load(Ge + t * 64 + lane);
+        const floatx4 v4 = MR_OP_GNT ? __builtin_nontemporal_load(Ge + t * 64 + lane) : Ge[t * 64 + lane];
         g[t] = make_float4(v4[0], v4[1], v4[2], v4[3]);
       }
       float d2 = 0.f;
@@ -2418,7 +2427,7 @@ int onepass_blocks_per_cu(bool user_side, int k) {
   return n;
 }
 
-int launch_cg_onepass(hipStream_t s, bool user_side, CgState* st, int update, int64_t E, int k,
+int launch_cg_onepass(hipStream_t s, bool user_side, CgState* st, int update, int rev, int64_t E, int k,
                       const float* G, const float* Gs, const float* Gn, double* p, double* pb,
                       double* r, double* rb, double* q, double* qb, float* x, float* xb,
                       int64_t* xbins, int n_part, CgMirror* mirror, int seq) {
@@ -2426,11 +2435,11 @@ int launch_cg_onepass(hipStream_t s, bool user_side, CgState* st, int update, in
 #define MR_OP_CASE(NB)                                                                      \
   case NB:                                                                                  \
     if (user_side)                                                                          \
-      MR_LAUNCH((cg_onepass_kernel<NB, true>), dim3(n_part), dim3(256), 0, s, st, update, E, \
-                k, ldk_of(k), G, Gs, Gn, p, pb, r, rb, q, qb, x, xb, xbins, mirror, seq);    \
+      MR_LAUNCH((cg_onepass_kernel<NB, true>), dim3(n_part), dim3(256), 0, s, st, update, rev, \
+                E, k, ldk_of(k), G, Gs, Gn, p, pb, r, rb, q, qb, x, xb, xbins, mirror, seq); \
     else                                                                                    \
       MR_LAUNCH((cg_onepass_kernel<NB, false>), dim3(n_part), dim3(256), 0, s, st, update,  \
-                E, k, ldk_of(k), G, Gs, Gn, p, pb, r, rb, q, qb, x, xb, xbins, mirror,     \
+                rev, E, k, ldk_of(k), G, Gs, Gn, p, pb, r, rb, q, qb, x, xb, xbins, mirror, \
                 seq);                                                                       \
     break;
   switch (nb16_of(k)) {

@@ -231,6 +231,38 @@ def test_replay_from_snapshot_is_bitwise_identical(gpu):
         assert np.array_equal(U, U1) and np.array_equal(V, V1)
 
 
+@pytest.mark.parametrize("k", [32, 64, 128])
+def test_cg_sweep_direction_is_bitwise_neutral(gpu, k):
+    """MR_OPT_CG_SWEEP only changes the order in which the one-pass kernel's
+    waves visit the entity chunks; every chunk's partial sums are
+    order-independent terms, so all three modes give identical CG counts
+    and bitwise-identical factors (k = 128: items one-pass, users
+    matvec + update)."""
+    from movie_recommender_amd import synth
+    from movie_recommender_amd.engine import AlsContext
+    # k = 128 at 2 % of the shape: most users rate fewer than 129 movies and
+    # the solves stop at once, so that case runs the full C4 shape
+    rs = synth.movielens_like("ml-full", k, scale=0.02 if k < 128 else 1.0)
+    rng = np.random.RandomState(1)
+    U0 = rng.uniform(-1, 1, rs.num_users * (k + 1))
+    V0 = rng.uniform(-1, 1, rs.num_items * k)
+    outs = []
+    with AlsContext(rs.user_ids, rs.item_ids, rs.ratings, k, rs.num_users,
+                    rs.num_items) as ctx:
+        for sweep in (0, 1, 2):
+            ctx.set_option("cg_sweep", sweep)
+            ctx.set_factors(U0, V0)
+            ctx.reset_stats()
+            ctx.iterate(3)
+            st = ctx.stats()
+            outs.append((ctx.get_factors(), st["cg_users_total"], st["cg_items_total"]))
+    (U1, V1), cu, ci = outs[0]
+    assert cu + ci > 6, (cu, ci)
+    for (U, V), cu2, ci2 in outs[1:]:
+        assert (cu2, ci2) == (cu, ci)
+        assert np.array_equal(U, U1) and np.array_equal(V, V1)
+
+
 @pytest.mark.parametrize("ratings", ["normal", "halfstar"])
 @pytest.mark.parametrize("k", [3, 10, 16, 20, 32, 33, 64, 65, 96, 128, 144, 200, 300])
 def test_gram_kernel_vs_numpy(gpu, k, ratings):
