@@ -138,9 +138,12 @@ struct CgLs {
     int32_t *rp32 = nullptr, *rowof = nullptr, *ci0 = nullptr;
     int64_t* rp0 = nullptr;
     double* v0 = nullptr;
-    if (dmalloc(&rp, rows + 1, owned) || dmalloc(&ci, nnz, owned) || dmalloc(&v, nnz, owned) ||
+    // ids / values padded by kSpPad entries: the SpMV's 16-byte row-block
+    // loads may run up to 7 entries past a block's (and the array's) end
+    if (dmalloc(&rp, rows + 1, owned) || dmalloc(&ci, nnz + kSpPad, owned) ||
+        dmalloc(&v, nnz + kSpPad, owned) ||
         dmalloc(&perm, rows, owned) || dmalloc(&tp, cols + 1, owned) ||
-        dmalloc(&ti, nnz, owned) || dmalloc(&tv, nnz, owned) || dmalloc(&b_in, rows, owned) ||
+        dmalloc(&ti, nnz + kSpPad, owned) || dmalloc(&tv, nnz + kSpPad, owned) || dmalloc(&b_in, rows, owned) ||
         dmalloc(&b, rows, owned) || dmalloc(&t, rows, owned) || dmalloc(&b2, cols, owned) ||
         dmalloc(&x, cols, owned) || dmalloc(&r, cols, owned) || dmalloc(&p, cols, owned) ||
         dmalloc(&q, cols, owned) || dmalloc(&partials, kMaxParts, owned) ||
@@ -203,12 +206,12 @@ struct CgLs {
   int iteration(int it, int sq) {
     if (tic(MR_CG_K_SPMV_A, it) ||
         launch_csr_spmv(s, it > 0 ? SPG_P : SPG_X, SPO_STORE, st, n_blk_a, blk_a, rp, ci, v,
-                        it > 0 ? r : p, p, t, nullptr, nullptr, 0, nullptr, kMaxParts,
+                        it > 0 ? r : p, p, cols, t, nullptr, nullptr, 0, nullptr, kMaxParts,
                         nullptr) ||
         toc())
       return -1;
     if (tic(MR_CG_K_SPMV_AT, it) ||
-        launch_csr_spmv(s, SPG_X, SPO_CG, st, n_blk_t, blk_t, tp, ti, tv, t, nullptr, q, p, r,
+        launch_csr_spmv(s, SPG_X, SPO_CG, st, n_blk_t, blk_t, tp, ti, tv, t, nullptr, rows, q, p, r,
                         it > 0 ? 1 : 0, partials, kMaxParts, st) ||
         toc())
       return -1;
@@ -239,10 +242,10 @@ struct CgLs {
     // b2 = A^T b (:463); r0 = A^T (A x) - b2, p0 = -r0, rr (:466-485)
     if (tic(MR_CG_K_SETUP, -1) ||
         launch_csr_spmv(s, SPG_X, SPO_STORE, nullptr, n_blk_t, blk_t, tp, ti, tv, b, nullptr,
-                        b2, nullptr, nullptr, 0, nullptr, kMaxParts, nullptr) ||
-        launch_csr_spmv(s, SPG_X, SPO_STORE, nullptr, n_blk_a, blk_a, rp, ci, v, x, nullptr, t,
+                        rows, b2, nullptr, nullptr, 0, nullptr, kMaxParts, nullptr) ||
+        launch_csr_spmv(s, SPG_X, SPO_STORE, nullptr, n_blk_a, blk_a, rp, ci, v, x, nullptr, cols, t,
                         nullptr, nullptr, 0, nullptr, kMaxParts, nullptr) ||
-        launch_csr_spmv(s, SPG_X, SPO_STORE, nullptr, n_blk_t, blk_t, tp, ti, tv, t, nullptr, q,
+        launch_csr_spmv(s, SPG_X, SPO_STORE, nullptr, n_blk_t, blk_t, tp, ti, tv, t, nullptr, rows, q,
                         nullptr, nullptr, 0, nullptr, kMaxParts, nullptr) ||
         launch_cgls_update(s, st, UPD_INIT, cols, x, r, p, q, b2, partials, kUpdParts, st,
                            d_mirror, ++seq) ||

@@ -3188,13 +3188,17 @@ int launch_predict(hipStream_t s, int64_t n, int k, int ldk, const int* uid,
 // r + alpha*q, sum += v*x.
 // ---------------------------------------------------------------------------
 constexpr int SP_THREADS = 256;
+#ifndef MR_SP_AUX   // cache policy of the once-read id / value streams (0: default; nt measured 4 % slower)
+#define MR_SP_AUX 0
+#endif
 constexpr int SP_TILE = kSpTile;     // staged products per row block (16 KiB fp64)
 
-template <int GATHER, int OUT>
+template <int GATHER, int OUT, bool BUF>
 __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
     const CgState* __restrict__ st, int64_t n_blk, const int64_t* __restrict__ blk,
     const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
     const double* __restrict__ v, const double* __restrict__ xa, const double* __restrict__ xb,
+    uint32_t xbytes,
     double* __restrict__ out, double* __restrict__ pv, const double* __restrict__ rv,
     int update_p, double* __restrict__ partials, CgState* fst) {
 #pragma clang fp contract(off)
@@ -3204,9 +3208,25 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
   __shared__ double sh[SP_THREADS / 64];
   const int t = threadIdx.x;
   double d = 0.0;   // OUT == SPO_CG: this thread's share of p.q
+  // BUF (gathered vectors < 4 GiB): buffer resources, so a load is a 32-bit
+  // offset from SGPR bases instead of 64-bit per-lane address arithmetic
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(xa), (short)0, (int)xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double*>(GATHER == SPG_P ? xb : xa), (short)0, (int)xbytes, 0x00020000);
+  auto ld_x = [&](const __amdgpu_buffer_rsrc_t& rs, const double* base, int32_t c) -> double {
+    if constexpr (BUF)
+      return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)((uint32_t)c * 8u), 0, 0));
+    else
+      return base[c];
+  };
   auto gather = [&](int32_t c) -> double {
-    if constexpr (GATHER == SPG_P) return -1.0 * xa[c] + beta * xb[c];
-    else return xa[c];
+#ifdef MR_SP_ONEGATHER   // timing probe only: wrong math
+    if constexpr (GATHER == SPG_P) { const double a = ld_x(ra, xa, c); return -1.0 * a + beta * a; }
+#else
+    if constexpr (GATHER == SPG_P) return -1.0 * ld_x(ra, xa, c) + beta * ld_x(rb, xb, c);
+#endif
+    else return ld_x(ra, xa, c);
   };
   auto emit = [&](int64_t row, double s) {
     out[row] = s;
@@ -3219,51 +3239,140 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
       d += pn * s;
     }
   };
-  for (int64_t b = blockIdx.x; b < n_blk; b += gridDim.x) {
-    const int64_t r0 = blk[b], r1 = blk[b + 1];
-    const int64_t n0 = rp[r0], n1 = rp[r1];
-    if (n1 - n0 <= SP_TILE) {
-      // all of a thread's column ids and values first, then all gathers, then
-      // the products: PER independent loads in flight per step instead of a
-      // dependent load -> gather chain per non-zero
-      constexpr int PER = SP_TILE / SP_THREADS;
-      int32_t cc[PER];
-      double vv[PER], gx[PER];
+  // Software pipeline over the workgroup's row blocks b, b + grid, ...: the
+  // next short block's column ids, values and row offsets are loaded into a
+  // second register set at the top of the current block (in flight during
+  // its gathers, products and sums), and block bounds (blk -> rp) are fetched
+  // two blocks ahead, so no load chain is exposed per block.  Products and
+  // row sums are unchanged: results are bitwise those of the plain loop.
+  constexpr int PER = SP_TILE / SP_THREADS;
+  __shared__ int32_t srp[kSpMaxRows + 1];   // the block's row offsets - n0
+  struct Stage {
+    int32_t cc[PER];
+    double vv[PER];
+    int32_t rpo;
+  };
+  auto load_short = [&](Stage& S, int64_t r0, int64_t r1, int64_t n0, int64_t n1) {
+    if constexpr (BUF) {
+      // thread t takes the block's entries 8t .. 8t+7 as 16-byte loads (two
+      // of ids, four of values; the arrays are padded by kSpPad entries, so
+      // no load leaves the allocation); entries past the block are read but
+      // never used (their products are not staged), and a gather of such an
+      // id is bounded by the vector's resource
+      // (resources end at the block's entry count rounded up to 8: every
+      // 16-byte load is wholly inside -- within the padding -- or wholly out
+      // of range, and out-of-range loads read 0 without touching memory)
+      const int n8 = ((int)(n1 - n0) + 7) & ~7;
+      const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<int32_t*>(ci + n0), (short)0, n8 * 4, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<double*>(v + n0), (short)0, n8 * 8, 0x00020000);
+      static_assert(PER == 8, "8 entries per thread");
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const u32x4_t c4 = __builtin_bit_cast(
+            u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rc, (8 * t + 4 * h) * 4, 0, MR_SP_AUX));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) S.cc[4 * h + i] = (int32_t)c4[i];
+      }
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const u32x4_t w4 = __builtin_bit_cast(
+            u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rw, (8 * t + 2 * h) * 8, 0, MR_SP_AUX));
+        S.vv[2 * h] = __builtin_bit_cast(double, ((uint64_t)w4[1] << 32) | w4[0]);
+        S.vv[2 * h + 1] = __builtin_bit_cast(double, ((uint64_t)w4[3] << 32) | w4[2]);
+      }
+    } else {
 #pragma unroll
       for (int u = 0; u < PER; ++u) {
         const int64_t j = n0 + t + (int64_t)u * SP_THREADS;
         const int64_t js = j < n1 ? j : 0;     // a valid address (arrays hold >= 1 entry)
         const int32_t c = ci[js];
-        vv[u] = v[js];
-        cc[u] = j < n1 ? c : 0;
+        S.vv[u] = v[js];
+        S.cc[u] = j < n1 ? c : 0;
       }
+    }
+    S.rpo = (t < r1 - r0) ? (int32_t)(rp[r0 + t] - n0) : 0;
+  };
+  Stage cur, nxt;
+  int64_t b = blockIdx.x;
+  const int64_t gs = gridDim.x;
+  int64_t r0 = 0, r1 = 0, n0 = 0, n1 = 0;      // block b
+  int64_t qr0 = 0, qr1 = 0, qn0 = 0, qn1 = 0;  // block b + gs
+  if (b < n_blk) {
+    r0 = blk[b];
+    r1 = blk[b + 1];
+    if (b + gs < n_blk) {
+      qr0 = blk[b + gs];
+      qr1 = blk[b + gs + 1];
+    }
+    n0 = rp[r0];
+    n1 = rp[r1];
+    if (b + gs < n_blk) {
+      qn0 = rp[qr0];
+      qn1 = rp[qr1];
+    }
+    if (n1 - n0 <= SP_TILE) load_short(cur, r0, r1, n0, n1);
+  }
+  for (; b < n_blk; b += gs) {
+    const bool has_next = b + gs < n_blk, has_next2 = b + 2 * gs < n_blk;
+    if (has_next && qn1 - qn0 <= SP_TILE) load_short(nxt, qr0, qr1, qn0, qn1);
+    int64_t sr0 = 0, sr1 = 0;   // bounds of block b + 2 gs
+    if (has_next2) {
+      sr0 = blk[b + 2 * gs];
+      sr1 = blk[b + 2 * gs + 1];
+    }
+    if (n1 - n0 <= SP_TILE) {
+      double gx[PER];
 #pragma unroll
-      for (int u = 0; u < PER; ++u) gx[u] = gather(cc[u]);
+      for (int u = 0; u < PER; ++u) gx[u] = gather(cur.cc[u]);
+      const int nl = (int)(n1 - n0);
 #pragma unroll
       for (int u = 0; u < PER; ++u) {
-        const int64_t j = n0 + t + (int64_t)u * SP_THREADS;
-        if (j < n1) prod[j - n0] = vv[u] * gx[u];
+        const int jl = BUF ? 8 * t + u : t + u * SP_THREADS;   // load_short's entry map
+        if (jl < nl) prod[jl] = cur.vv[u] * gx[u];
       }
-      __syncthreads();
       const int R = (int)(r1 - r0);
+      if (t < R) srp[t] = cur.rpo;
+      if (t == 0) srp[R] = (int32_t)(n1 - n0);
+      __syncthreads();
       int G = 1;
       while (G < 64 && 2 * G * R <= SP_THREADS) G *= 2;
       const int lr = t / G, g = t & (G - 1);
-      double s = 0.0;
+      double sum = 0.0;
       if (lr < R) {
-        const int64_t e = rp[r0 + lr + 1] - n0;
-        for (int64_t j = rp[r0 + lr] - n0 + g; j < e; j += G) s += prod[j];
+        const int e = srp[lr + 1];
+        const int j0 = srp[lr] + g;
+        if (j0 + 15 * G >= e) {
+          // <= 16 terms: all LDS reads issued first, then the adds in order
+          double pv16[16];
+#pragma unroll
+          for (int i = 0; i < 16; ++i) pv16[i] = (j0 + i * G < e) ? prod[j0 + i * G] : 0.0;
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (j0 + i * G < e) sum += pv16[i];
+        } else {
+          for (int j = j0; j < e; j += G) sum += prod[j];
+        }
       }
-      for (int o = G / 2; o > 0; o >>= 1) s += __shfl_xor(s, o);
-      if (lr < R && g == 0) emit(r0 + lr, s);
-      __syncthreads();   // prod is reused by the next block
+      for (int o = G / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+      if (lr < R && g == 0) emit(r0 + lr, sum);
+      __syncthreads();   // prod / srp are reused by the next block
     } else {             // one long row: per-thread strided sums, fixed-order tree
-      double s = 0.0;
-      for (int64_t j = n0 + t; j < n1; j += SP_THREADS) s += v[j] * gather(ci[j]);
-      s = block_sum_f64<SP_THREADS>(s, sh);
-      if (t == 0) emit(r0, s);
+      double sum = 0.0;
+      for (int64_t j = n0 + t; j < n1; j += SP_THREADS) sum += v[j] * gather(ci[j]);
+      sum = block_sum_f64<SP_THREADS>(sum, sh);
+      if (t == 0) emit(r0, sum);
       __syncthreads();
     }
+    int64_t sn0 = 0, sn1 = 0;
+    if (has_next2) {
+      sn0 = rp[sr0];
+      sn1 = rp[sr1];
+    }
+    r0 = qr0; r1 = qr1; n0 = qn0; n1 = qn1;
+    qr0 = sr0; qr1 = sr1; qn0 = sn0; qn1 = sn1;
+    cur = nxt;
   }
   if constexpr (OUT == SPO_CG) {
     const double tot = block_sum_f64<SP_THREADS>(d, sh);
@@ -3278,14 +3387,45 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
 
 int launch_csr_spmv(hipStream_t s, int gather, int out_mode, const CgState* st, int64_t n_blk,
                     const int64_t* blk, const int64_t* rp, const int32_t* ci, const double* v,
-                    const double* xa, const double* xb, double* out, double* pv,
+                    const double* xa, const double* xb, int64_t nx, double* out, double* pv,
                     const double* rv, int update_p, double* partials, int n_part,
                     CgState* fst) {
   if (n_blk <= 0) return 0;
-  const dim3 grid((unsigned)std::min<int64_t>(n_blk, n_part));
+  // at most the workgroups the chip holds at once: a fixed grid larger than
+  // that runs a second, partial round of grid-stride loops (general CG at
+  // 27e6 x 2.8e6: 2,048 blocks at 5 per CU measured slower than 1,280)
+  static const int cus = [] {
+    int d = 0, n = 0;
+    if (hipGetDevice(&d) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+      return 0;
+    return n;
+  }();
+  const bool buf = nx >= 0 && nx * 8 < (int64_t)0xFFFFFFF0;
+  const void* fn = nullptr;
+#define MR_SP_FN(GA, OU)                                                                   \
+  fn = buf ? (const void*)csr_spmv_kernel<GA, OU, true> : (const void*)csr_spmv_kernel<GA, OU, false>
+  if (out_mode == SPO_CG) {
+    if (gather == SPG_P) MR_SP_FN(SPG_P, SPO_CG);
+    else MR_SP_FN(SPG_X, SPO_CG);
+  } else {
+    if (gather == SPG_P) MR_SP_FN(SPG_P, SPO_STORE);
+    else MR_SP_FN(SPG_X, SPO_STORE);
+  }
+#undef MR_SP_FN
+  int bpc = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, SP_THREADS, 0) != hipSuccess) bpc = 0;
+  int64_t parts = n_part;
+  if (bpc > 0 && cus > 0) parts = std::min<int64_t>(parts, (int64_t)bpc * cus);
+  const dim3 grid((unsigned)std::min<int64_t>(n_blk, parts));
+  const uint32_t xbytes = buf ? (uint32_t)(nx * 8) : 0u;
 #define MR_SP(GA, OU)                                                                      \
-  MR_LAUNCH((csr_spmv_kernel<GA, OU>), grid, dim3(SP_THREADS), 0, s, st, n_blk, blk, rp, ci, \
-            v, xa, xb, out, pv, rv, update_p, partials, fst)
+  if (buf)                                                                                  \
+    MR_LAUNCH((csr_spmv_kernel<GA, OU, true>), grid, dim3(SP_THREADS), 0, s, st, n_blk, blk, \
+              rp, ci, v, xa, xb, xbytes, out, pv, rv, update_p, partials, fst);            \
+  else                                                                                      \
+    MR_LAUNCH((csr_spmv_kernel<GA, OU, false>), grid, dim3(SP_THREADS), 0, s, st, n_blk,    \
+              blk, rp, ci, v, xa, xb, xbytes, out, pv, rv, update_p, partials, fst)
   if (out_mode == SPO_CG) {
     if (gather == SPG_P) MR_SP(SPG_P, SPO_CG);
     else MR_SP(SPG_X, SPO_CG);

@@ -343,12 +343,13 @@ int launch_predict(hipStream_t s, int64_t n, int k, int ldk, const int* uid,
 enum SpGather { SPG_X = 0, SPG_P = 1 };
 enum SpOut { SPO_STORE = 0, SPO_CG = 1 };
 constexpr int kSpTile = 2048;
+constexpr int kSpPad = 16;   // entries past nnz every SpMV id / value array holds
 constexpr int kSpMaxRows = 256;
 int launch_csr_spmv(hipStream_t s, int gather, int out_mode, const CgState* st, int64_t n_blk,
                     const int64_t* blk, const int64_t* rp, const int32_t* ci, const double* v,
-                    const double* xa, const double* xb, double* out, double* pv,
+                    const double* xa, const double* xb, int64_t nx, double* out, double* pv,
                     const double* rv, int update_p, double* partials, int n_part,
-                    CgState* fst);
+                    CgState* fst);   // nx: length of the gathered vector(s) xa / xb
 int launch_cgls_update(hipStream_t s, const CgState* st, int mode, int64_t n, double* x,
                        double* r, double* p, const double* q, const double* b2,
                        double* partials, int n_part, CgState* fst, CgMirror* mirror, int seq);
