@@ -3221,11 +3221,7 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
       return base[c];
   };
   auto gather = [&](int32_t c) -> double {
-#ifdef MR_SP_ONEGATHER   // timing probe only: wrong math
-    if constexpr (GATHER == SPG_P) { const double a = ld_x(ra, xa, c); return -1.0 * a + beta * a; }
-#else
     if constexpr (GATHER == SPG_P) return -1.0 * ld_x(ra, xa, c) + beta * ld_x(rb, xb, c);
-#endif
     else return ld_x(ra, xa, c);
   };
   auto emit = [&](int64_t row, double s) {
