@@ -62,7 +62,8 @@ struct CgLs {
   int64_t n_blk_a = 0, n_blk_t = 0;
   int32_t *ci = nullptr, *ti = nullptr, *perm = nullptr;
   double *v = nullptr, *tv = nullptr;
-  double *b_in = nullptr, *b = nullptr, *b2 = nullptr, *x = nullptr, *r = nullptr, *p = nullptr, *q = nullptr,
+  // rp: the CG's r and p interleaved (rp[2j] = r_j, rp[2j+1] = p_j)
+  double *b_in = nullptr, *b = nullptr, *b2 = nullptr, *x = nullptr, *rp2 = nullptr, *q = nullptr,
          *t = nullptr, *partials = nullptr;
   CgState* st = nullptr;
   CgState* h_init = nullptr;
@@ -145,7 +146,7 @@ struct CgLs {
         dmalloc(&perm, rows, owned) || dmalloc(&tp, cols + 1, owned) ||
         dmalloc(&ti, nnz + kSpPad, owned) || dmalloc(&tv, nnz + kSpPad, owned) || dmalloc(&b_in, rows, owned) ||
         dmalloc(&b, rows, owned) || dmalloc(&t, rows, owned) || dmalloc(&b2, cols, owned) ||
-        dmalloc(&x, cols, owned) || dmalloc(&r, cols, owned) || dmalloc(&p, cols, owned) ||
+        dmalloc(&x, cols, owned) || dmalloc(&rp2, 2 * cols, owned) ||
         dmalloc(&q, cols, owned) || dmalloc(&partials, kMaxParts, owned) ||
         dmalloc(&st, 1, owned))
       return -1;
@@ -205,18 +206,18 @@ struct CgLs {
   // update and alpha; x, r update with the BETA rule, published under `sq`.
   int iteration(int it, int sq) {
     if (tic(MR_CG_K_SPMV_A, it) ||
-        launch_csr_spmv(s, it > 0 ? SPG_P : SPG_X, SPO_STORE, st, n_blk_a, blk_a, rp, ci, v,
-                        it > 0 ? r : p, p, cols, t, nullptr, nullptr, 0, nullptr, kMaxParts,
+        launch_csr_spmv(s, it > 0 ? SPG_P : SPG_P0, SPO_STORE, st, n_blk_a, blk_a, rp, ci, v,
+                        rp2, nullptr, 2 * cols, t, nullptr, nullptr, 0, nullptr, kMaxParts,
                         nullptr) ||
         toc())
       return -1;
     if (tic(MR_CG_K_SPMV_AT, it) ||
-        launch_csr_spmv(s, SPG_X, SPO_CG, st, n_blk_t, blk_t, tp, ti, tv, t, nullptr, rows, q, p, r,
+        launch_csr_spmv(s, SPG_X, SPO_CG, st, n_blk_t, blk_t, tp, ti, tv, t, nullptr, rows, q, rp2, nullptr,
                         it > 0 ? 1 : 0, partials, kMaxParts, st) ||
         toc())
       return -1;
     if (tic(MR_CG_K_UPDATE, it) ||
-        launch_cgls_update(s, st, UPD_STEP, cols, x, r, p, q, b2, partials, kUpdParts, st,
+        launch_cgls_update(s, st, UPD_STEP, cols, x, rp2, q, b2, partials, kUpdParts, st,
                            d_mirror, sq) ||
         toc())
       return -1;
@@ -247,7 +248,7 @@ struct CgLs {
                         nullptr, nullptr, 0, nullptr, kMaxParts, nullptr) ||
         launch_csr_spmv(s, SPG_X, SPO_STORE, nullptr, n_blk_t, blk_t, tp, ti, tv, t, nullptr, rows, q,
                         nullptr, nullptr, 0, nullptr, kMaxParts, nullptr) ||
-        launch_cgls_update(s, st, UPD_INIT, cols, x, r, p, q, b2, partials, kUpdParts, st,
+        launch_cgls_update(s, st, UPD_INIT, cols, x, rp2, q, b2, partials, kUpdParts, st,
                            d_mirror, ++seq) ||
         toc())
       return -1;

@@ -3204,6 +3204,7 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
 #pragma clang fp contract(off)
   if (st && ald(&st->done)) return;
   const double beta = (st && (GATHER == SPG_P || update_p)) ? ald(&st->beta) : 0.0;
+  static_assert(OUT != SPO_CG || GATHER == SPG_X, "the CG output pass gathers t");
   __shared__ double prod[SP_TILE];
   __shared__ double sh[SP_THREADS / 64];
   const int t = threadIdx.x;
@@ -3212,25 +3213,29 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
   // offset from SGPR bases instead of 64-bit per-lane address arithmetic
   const __amdgpu_buffer_rsrc_t ra =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(xa), (short)0, (int)xbytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<double*>(GATHER == SPG_P ? xb : xa), (short)0, (int)xbytes, 0x00020000);
-  auto ld_x = [&](const __amdgpu_buffer_rsrc_t& rs, const double* base, int32_t c) -> double {
-    if constexpr (BUF)
-      return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)((uint32_t)c * 8u), 0, 0));
-    else
-      return base[c];
-  };
   auto gather = [&](int32_t c) -> double {
-    if constexpr (GATHER == SPG_P) return -1.0 * ld_x(ra, xa, c) + beta * ld_x(rb, xb, c);
-    else return ld_x(ra, xa, c);
+    if constexpr (GATHER == SPG_P) {   // p_c = -r_c + beta p_c from one 16-byte (r, p) pair
+      double2 w;
+      if constexpr (BUF)
+        w = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(ra, (int)((uint32_t)c * 16u), 0, 0));
+      else
+        w = reinterpret_cast<const double2*>(xa)[c];
+      return -1.0 * w.x + beta * w.y;
+    } else {
+      const uint32_t i = GATHER == SPG_P0 ? 2u * (uint32_t)c + 1u : (uint32_t)c;
+      if constexpr (BUF)
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(ra, (int)(i * 8u), 0, 0));
+      else
+        return xa[GATHER == SPG_P0 ? 2 * (int64_t)c + 1 : (int64_t)c];
+    }
   };
   auto emit = [&](int64_t row, double s) {
     out[row] = s;
-    if constexpr (OUT == SPO_CG) {
-      double pn = pv[row];
+    if constexpr (OUT == SPO_CG) {   // pv = the interleaved (r, p) pairs
+      double pn = pv[2 * row + 1];
       if (update_p) {
-        pn = -1.0 * rv[row] + beta * pn;   // vect_add(-1, r, beta, p, p)
-        pv[row] = pn;
+        pn = -1.0 * pv[2 * row] + beta * pn;   // vect_add(-1, r, beta, p, p)
+        pv[2 * row + 1] = pn;
       }
       d += pn * s;
     }
@@ -3402,10 +3407,14 @@ int launch_csr_spmv(hipStream_t s, int gather, int out_mode, const CgState* st, 
 #define MR_SP_FN(GA, OU)                                                                   \
   fn = buf ? (const void*)csr_spmv_kernel<GA, OU, true> : (const void*)csr_spmv_kernel<GA, OU, false>
   if (out_mode == SPO_CG) {
-    if (gather == SPG_P) MR_SP_FN(SPG_P, SPO_CG);
-    else MR_SP_FN(SPG_X, SPO_CG);
+    if (gather != SPG_X) {
+      set_error("the CG output pass gathers a plain vector");
+      return -1;
+    }
+    MR_SP_FN(SPG_X, SPO_CG);
   } else {
     if (gather == SPG_P) MR_SP_FN(SPG_P, SPO_STORE);
+    else if (gather == SPG_P0) MR_SP_FN(SPG_P0, SPO_STORE);
     else MR_SP_FN(SPG_X, SPO_STORE);
   }
 #undef MR_SP_FN
@@ -3423,10 +3432,10 @@ int launch_csr_spmv(hipStream_t s, int gather, int out_mode, const CgState* st, 
     MR_LAUNCH((csr_spmv_kernel<GA, OU, false>), grid, dim3(SP_THREADS), 0, s, st, n_blk,    \
               blk, rp, ci, v, xa, xb, xbytes, out, pv, rv, update_p, partials, fst)
   if (out_mode == SPO_CG) {
-    if (gather == SPG_P) MR_SP(SPG_P, SPO_CG);
-    else MR_SP(SPG_X, SPO_CG);
+    MR_SP(SPG_X, SPO_CG);
   } else {
     if (gather == SPG_P) MR_SP(SPG_P, SPO_STORE);
+    else if (gather == SPG_P0) MR_SP(SPG_P0, SPO_STORE);
     else MR_SP(SPG_X, SPO_STORE);
   }
 #undef MR_SP
@@ -3440,7 +3449,7 @@ int launch_csr_spmv(hipStream_t s, int gather, int out_mode, const CgState* st, 
 // rule and publishes the state.
 __global__ __launch_bounds__(256) void cgls_update_kernel(
     const CgState* __restrict__ st, int mode, int64_t n, double* __restrict__ x,
-    double* __restrict__ r, double* __restrict__ p, const double* __restrict__ q,
+    double2* __restrict__ rp, const double* __restrict__ q,
     const double* __restrict__ b2, double* __restrict__ partials, CgState* fst,
     CgMirror* mirror, int seq) {
 #pragma clang fp contract(off)
@@ -3450,15 +3459,17 @@ __global__ __launch_bounds__(256) void cgls_update_kernel(
   double acc = 0.0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    double rv;
+    double rv, pv;
     if (mode == UPD_INIT) {
       rv = 1.0 * q[i] + -1.0 * b2[i];
-      p[i] = -1.0 * rv;
+      pv = -1.0 * rv;
     } else {
-      x[i] = 1.0 * x[i] + alpha * p[i];
-      rv = 1.0 * r[i] + alpha * q[i];
+      const double2 w = rp[i];   // (r, p)
+      pv = w.y;
+      x[i] = 1.0 * x[i] + alpha * pv;
+      rv = 1.0 * w.x + alpha * q[i];
     }
-    r[i] = rv;
+    rp[i] = make_double2(rv, pv);
     acc += rv * rv;
   }
   const double tot = block_sum_f64<256>(acc, sh);
@@ -3467,10 +3478,10 @@ __global__ __launch_bounds__(256) void cgls_update_kernel(
 }
 
 int launch_cgls_update(hipStream_t s, const CgState* st, int mode, int64_t n, double* x,
-                       double* r, double* p, const double* q, const double* b2,
+                       double* rp, const double* q, const double* b2,
                        double* partials, int n_part, CgState* fst, CgMirror* mirror, int seq) {
-  MR_LAUNCH(cgls_update_kernel, dim3(n_part), dim3(256), 0, s, st, mode, n, x, r, p, q, b2,
-            partials, fst, mirror, seq);
+  MR_LAUNCH(cgls_update_kernel, dim3(n_part), dim3(256), 0, s, st, mode, n, x,
+            reinterpret_cast<double2*>(rp), q, b2, partials, fst, mirror, seq);
   MR_HIP(hipGetLastError());
   return 0;
 }

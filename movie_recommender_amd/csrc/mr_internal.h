@@ -336,11 +336,13 @@ int launch_predict(hipStream_t s, int64_t n, int k, int ldk, const int* uid,
 // General CSR (fp64) CG least squares (cg_least_squares_from_python):
 // CSR-stream SpMV over row blocks blk[0..n_blk] (consecutive rows with
 // <= 2048 non-zeros, <= 256 rows, or one longer row), fixed grid of
-// min(n_blk, n_part) workgroups.  gather SPG_X: x_c = xa[c]; SPG_P: p_c =
-// -xa[c] + beta xb[c] (xa = r, xb = p).  out SPO_STORE: out[row] = sum;
-// SPO_CG: out[row] = q_row, p_row updated in pv (update_p) and p.q summed,
-// the last workgroup computes alpha (fst, partials[n_part]).
-enum SpGather { SPG_X = 0, SPG_P = 1 };
+// min(n_blk, n_part) workgroups.  The CG's r and p live interleaved, rp[2j]
+// = r_j, rp[2j+1] = p_j (one 16-byte gather per non-zero).  gather SPG_X:
+// x_c = xa[c]; SPG_P: p_c = -r_c + beta p_c from xa = rp; SPG_P0: p_c from
+// xa = rp.  out SPO_STORE: out[row] = sum; SPO_CG: out[row] = q_row, p_row
+// updated in pv = rp (update_p) and p.q summed, the last workgroup computes
+// alpha (fst, partials[n_part]).  nx: doubles in the gathered array.
+enum SpGather { SPG_X = 0, SPG_P = 1, SPG_P0 = 2 };
 enum SpOut { SPO_STORE = 0, SPO_CG = 1 };
 constexpr int kSpTile = 2048;
 constexpr int kSpPad = 16;   // entries past nnz every SpMV id / value array holds
@@ -351,7 +353,7 @@ int launch_csr_spmv(hipStream_t s, int gather, int out_mode, const CgState* st, 
                     const double* rv, int update_p, double* partials, int n_part,
                     CgState* fst);   // nx: length of the gathered vector(s) xa / xb
 int launch_cgls_update(hipStream_t s, const CgState* st, int mode, int64_t n, double* x,
-                       double* r, double* p, const double* q, const double* b2,
+                       double* rp, const double* q, const double* b2,
                        double* partials, int n_part, CgState* fst, CgMirror* mirror, int seq);
 int launch_rows_of(hipStream_t s, int64_t rows, const int64_t* rp,
                    int32_t* row_of);
