@@ -1070,22 +1070,26 @@ int Engine::cg_onepass(Side& S, double min_dec, int max_it, double* final_rr, bo
   int launched = 0;          // iteration kernels enqueued (t = 0 .. launched-1)
   CgMirror ms{};
   if (started) {
-    if (S.n_split) {
-      const CgStart cs = cg_start_of(S);
+    // INIT rule, alpha_0 and iteration 0's BETA step (its update deferred):
+    // by the last block of the split entities' start when there are any
+    // (the CG_START control folded in, one launch less), else by the control
+    seq_of.push_back(++mirror_seq);
+    const CgStart cs = cg_start_of(S);
+    if (S.n_split && cs.xbins) {
+      StartFold fold{d_state, d_mirror, seq_of[0], min_dec, max_it, 2};
       if (tic(MR_K_CG_START, -1, &a)) return -1;
       if (launch_cg_start_split(stream, user, k, S.split, S.n_split, direct_dst(S), cs,
-                                S.start_parts + 3 * gram_blocks(S.n_work)))
+                                S.start_parts + 3 * gram_blocks(S.n_work), fold))
         return -1;
       if (toc(MR_K_CG_START, -1, a)) return -1;
+    } else {
+      if (tic(MR_K_CG_CONTROL, -1, &a)) return -1;
+      if (launch_cg_control(stream, d_state, CG_START, CTL_BOTH, S.start_parts,
+                            (int)S.n_start_pairs, d_mirror, seq_of[0], min_dec, max_it, 2,
+                            xbins + kXBinWords))
+        return -1;
+      if (toc(MR_K_CG_CONTROL, -1, a)) return -1;
     }
-    // INIT rule, alpha_0 and iteration 0's BETA step (its update deferred)
-    seq_of.push_back(++mirror_seq);
-    if (tic(MR_K_CG_CONTROL, -1, &a)) return -1;
-    if (launch_cg_control(stream, d_state, CG_START, CTL_BOTH, S.start_parts,
-                          (int)S.n_start_pairs, d_mirror, seq_of[0], min_dec, max_it, 2,
-                          xbins + kXBinWords))
-      return -1;
-    if (toc(MR_K_CG_CONTROL, -1, a)) return -1;
     launched = 1;
   } else {
     MR_HIP(hipMemcpyAsync(d_state, h_init, sizeof(CgState), hipMemcpyHostToDevice, stream));

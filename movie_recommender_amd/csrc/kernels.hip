@@ -1224,11 +1224,16 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 3 : 1)) void gram_kernel(
 }
 
 // Split entities: the CG start after slab_reduce (one wave per entity).
+// the folded CG_START control, run by wave 0 of cg_start_split's last block
+// (defined with the control kernel below)
+__device__ void start_fold_finalize(const StartFold& f, int64_t* start_xbins);
+
 template <int NB, bool USER>
 __global__ __launch_bounds__(256) void cg_start_split_kernel(const SplitItem* __restrict__ split,
                                                              int64_t n_split, int k, int ldk,
                                                              GramDst direct, CgStart cs,
-                                                             double* __restrict__ parts) {
+                                                             double* __restrict__ parts,
+                                                             StartFold fold) {
   __shared__ MvScratch<NB> scr[4];
   const int wid = threadIdx.x >> 6;
   const int64_t i = (int64_t)blockIdx.x * 4 + wid;
@@ -1239,6 +1244,19 @@ __global__ __launch_bounds__(256) void cg_start_split_kernel(const SplitItem* __
     const int lane = threadIdx.x & 63;
     const int64_t t3[3] = {xterm(drr, lane), xterm(dpq, lane), xterm(dqq, lane)};
     xsum_flush<3>(t3, cs.xbins);
+    if (fold.st) {
+      // last-arriving block: every block's bin atomics are drained (vmcnt)
+      // before its arrival add, as in the one-pass kernel's hand-off
+      __shared__ int s_last;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's bin atomics
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        s_last = __hip_atomic_fetch_add(&fold.st->arrive_start, 1u, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+      }
+      __syncthreads();
+      if (s_last && wid == 0) start_fold_finalize(fold, cs.xbins);
+    }
   } else {
     store_start_sums(drr, dpq, dqq, parts);
   }
@@ -1598,7 +1616,8 @@ int launch_gram(hipStream_t s, bool user_side, int k, const WorkItem* work,
 }
 
 int launch_cg_start_split(hipStream_t s, bool user_side, int k, const SplitItem* split,
-                          int64_t n_split, GramDst direct, const CgStart& cs, double* parts) {
+                          int64_t n_split, GramDst direct, const CgStart& cs, double* parts,
+                          const StartFold& fold) {
   if (n_split <= 0) return 0;
   const unsigned grid = (unsigned)((n_split + 3) / 4);
   const int ldk = ldk_of(k);
@@ -1606,10 +1625,10 @@ int launch_cg_start_split(hipStream_t s, bool user_side, int k, const SplitItem*
   case NB:                                                                                  \
     if (user_side)                                                                          \
       MR_LAUNCH((cg_start_split_kernel<NB, true>), dim3(grid), dim3(256), 0, s, split, n_split, \
-                k, ldk, direct, cs, parts);                                                 \
+                k, ldk, direct, cs, parts, fold);                                           \
     else                                                                                    \
       MR_LAUNCH((cg_start_split_kernel<NB, false>), dim3(grid), dim3(256), 0, s, split,     \
-                n_split, k, ldk, direct, cs, parts);                                        \
+                n_split, k, ldk, direct, cs, parts, fold);                                  \
     break;
   switch (nb16_of(k)) {
     MR_SS_CASE(1) MR_SS_CASE(2) MR_SS_CASE(3) MR_SS_CASE(4)
@@ -2769,6 +2788,11 @@ __global__ void x_to_vec_kernel(int64_t n, int64_t nb, const float* __restrict__
 // all-reduce that slot next); CTL_FINALIZE applies the rules from comm[0].
 // ---------------------------------------------------------------------------
 
+__device__ bool start_reduce_xbins(CgState* st, int64_t* start_xbins, bool exchange,
+                                   CgMirror* mirror, int seq);
+__device__ void start_rule(CgState* st, CgMirror* mirror, int seq, double min_dec, int max_it,
+                           int sharded);
+
 constexpr int CTL_THREADS = 1024;
 __global__ __launch_bounds__(CTL_THREADS) void cg_control_kernel(
     CgState* __restrict__ st, int phase, int ctl,
@@ -2781,25 +2805,7 @@ __global__ __launch_bounds__(CTL_THREADS) void cg_control_kernel(
       // one-pass CG: the start's sums from the order-independent bins (wave
       // 0), exchanged as integers with the peers, then to fp64
       if (threadIdx.x >= 64) return;
-      const int lane = threadIdx.x;
-      __shared__ int64_t xs[3 * kXW];
-      int64_t t = xsum_collect<3>(start_xbins, lane);
-      PeerComm* pc = ald(&st->peer);
-      if (pc && (ctl & CTL_FINALIZE) && !peer_sum_lanes(pc, t, 3 * kXW)) {
-        if (lane == 0) {
-          ast(&st->comm[0], 0.0);
-          ast(&st->comm[1], 0.0);
-          peer_fail(st, mirror, seq);
-        }
-        return;
-      }
-      if (lane < 3 * kXW) xs[lane] = t;
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0) {
-        ast(&st->comm[0], xsum_value(&xs[0]));
-        ast(&st->comm[1], xsum_value(&xs[kXW]));
-        ast(&st->comm[2], xsum_value(&xs[2 * kXW]));
-      }
+      if (!start_reduce_xbins(st, start_xbins, (ctl & CTL_FINALIZE) != 0, mirror, seq)) return;
     } else if (phase == CG_START) {
       // (r.r, p.Gp, q.q) triples (one per Gram block: ~E/4 of them, written
       // by every XCD): thread t sums triples t, t + T, t + 2T, ... in order,
@@ -2847,8 +2853,54 @@ __global__ __launch_bounds__(CTL_THREADS) void cg_control_kernel(
   }
   if (threadIdx.x != 0 || !(ctl & CTL_FINALIZE)) return;
   if (phase == CG_START) {
-    // fresh state (cg_least_squares entry), then the INIT rule on r0.r0 and,
-    // unless that ended the solve, alpha of iteration 0 from p0.G p0
+    start_rule(st, mirror, seq, min_dec, max_it, sharded);
+    return;
+  }
+  cg_finalize(st, phase, ald(&st->comm[0]), mirror, seq);
+}
+
+// The start's three sums from the order-independent bins, by one wave: peers
+// exchange the integer containers (when `exchange` and sharded), lane 0
+// stores the fp64 values into comm[0..2].  False on a peer timeout (the state
+// is then failed and published).
+__device__ bool start_reduce_xbins(CgState* st, int64_t* start_xbins, bool exchange,
+                                   CgMirror* mirror, int seq) {
+  const int lane = threadIdx.x & 63;
+  __shared__ int64_t xs[3 * kXW];
+  int64_t t = xsum_collect<3>(start_xbins, lane);
+  PeerComm* pc = ald(&st->peer);
+  if (pc && exchange && !peer_sum_lanes(pc, t, 3 * kXW)) {
+    if (lane == 0) {
+      ast(&st->comm[0], 0.0);
+      ast(&st->comm[1], 0.0);
+      peer_fail(st, mirror, seq);
+    }
+    return false;
+  }
+  if (lane < 3 * kXW) xs[lane] = t;
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) {
+    ast(&st->comm[0], xsum_value(&xs[0]));
+    ast(&st->comm[1], xsum_value(&xs[kXW]));
+    ast(&st->comm[2], xsum_value(&xs[2 * kXW]));
+  }
+  return true;
+}
+
+__device__ void start_fold_finalize(const StartFold& f, int64_t* start_xbins) {
+  // the counter is reset first, so a failed peer exchange leaves it clean too
+  if ((threadIdx.x & 63) == 0)
+    __hip_atomic_store(&f.st->arrive_start, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!start_reduce_xbins(f.st, start_xbins, true, f.mirror, f.seq)) return;
+  if ((threadIdx.x & 63) == 0) start_rule(f.st, f.mirror, f.seq, f.min_dec, f.max_it, f.sharded);
+}
+
+// CG_START rule, by one thread: fresh state (cg_least_squares entry), then
+// the INIT rule on r0.r0 and, unless that ended the solve, alpha of
+// iteration 0 from p0.G p0 (comm[0..2] hold r0.r0, p0.q0, q0.q0)
+__device__ void start_rule(CgState* st, CgMirror* mirror, int seq, double min_dec, int max_it,
+                           int sharded) {
+  {
     CgScalars v;
     const double rr = ald(&st->comm[0]), pq = ald(&st->comm[1]);
     const int onepass = (sharded >> 1) & 1;   // bit 1 of the argument
@@ -2885,9 +2937,7 @@ __global__ __launch_bounds__(CTL_THREADS) void cg_control_kernel(
     }
     store_state(st, v);
     publish(v, mirror, seq);
-    return;
   }
-  cg_finalize(st, phase, ald(&st->comm[0]), mirror, seq);
 }
 
 int launch_cg_control(hipStream_t s, CgState* st, int phase, int ctl,

@@ -223,6 +223,18 @@ struct CgState {
   int32_t onepass;  // one kernel per CG iteration (cg_matvec_kernel, DESIGN.md
                     // "One-pass CG iteration"); set by the host per solve
   int32_t pending;  // one-pass: the last iteration's x / r update is not applied yet
+  uint32_t arrive_start;  // cg_start_split blocks finished (folded CG_START control)
+};
+// The CG_START control folded into cg_start_split's last block (one-pass
+// solves with split entities): st == nullptr keeps the separate control launch.
+struct CgMirror;
+struct StartFold {
+  CgState* st;
+  CgMirror* mirror;
+  int seq;
+  double min_dec;
+  int max_it;
+  int sharded;   // cg_control's `sharded` argument (bit 1: one-pass)
 };
 
 // Host-visible copies of the CG state: a ring of kMirrorSlots records in
@@ -262,7 +274,8 @@ int launch_gram(hipStream_t s, bool user_side, int k, const WorkItem* work,
                 GramDst slab, const CgStart* start = nullptr, bool rhs_mfma = false);
 inline int64_t gram_blocks(int64_t n_work) { return (n_work + 3) / 4; }
 int launch_cg_start_split(hipStream_t s, bool user_side, int k, const SplitItem* split,
-                          int64_t n_split, GramDst direct, const CgStart& cs, double* parts);
+                          int64_t n_split, GramDst direct, const CgStart& cs, double* parts,
+                          const StartFold& fold = StartFold{});
 int launch_slab_reduce(hipStream_t s, bool user_side, int k,
                        const SplitItem* split, int64_t n_split,
                        const float* slab, int64_t rec, GramDst direct);
