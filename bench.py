@@ -508,11 +508,19 @@ def main():
         out["cpu_baseline"] = None
     ctx.close()
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        os.write(JSON_FD, (json.dumps(out) + "\n").encode())
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
 
 
+# The contract's ONE JSON line goes to the original stdout; everything else a
+# library writes to fd 1 (RCCL prints a version banner on communicator init)
+# is redirected to stderr, so stdout carries nothing but that line.
+JSON_FD = 1
+
 if __name__ == "__main__":
+    sys.stdout.flush()
+    JSON_FD = os.dup(1)
+    os.dup2(2, 1)
     main()
