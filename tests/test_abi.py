@@ -106,3 +106,13 @@ def test_reference_wrapper_calling_convention(gpu):
                                           ctypes.byref(final_rr))
     assert it == int(g["iterations"])
     assert rel_err(x.ravel(), g["x"]) <= 1e-9
+
+
+def test_engine_option_table_matches_header():
+    """engine.OPTIONS (the names set_option accepts) is exactly the
+    MR_OPT_* enum of include/mr_als.h."""
+    from movie_recommender_amd.engine import OPTIONS
+    src = open(os.path.join(ROOT, "include", "mr_als.h")).read()
+    enum = {m.group(1).lower(): int(m.group(2))
+            for m in re.finditer(r"MR_OPT_(\w+)\s*=\s*(\d+)", src)}
+    assert OPTIONS == enum
