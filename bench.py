@@ -47,13 +47,14 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def load_data(shape, k, cache_dir="/tmp"):
-    path = os.path.join(cache_dir, f"mr_bench_{shape}_k{k}_{synth.DATA_SEED}.npz")
+def load_data(shape, k, cache_dir="/tmp", scale=1.0):
+    tag = "" if scale == 1.0 else f"_x{scale:g}"
+    path = os.path.join(cache_dir, f"mr_bench_{shape}{tag}_k{k}_{synth.DATA_SEED}.npz")
     if os.path.exists(path):
         with np.load(path, allow_pickle=False) as d:
             rs = synth.RatingSet(d["u"], d["i"], d["r"], int(d["nu"]), int(d["ni"]), k)
             return rs
-    rs = synth.movielens_like(shape, k)
+    rs = synth.movielens_like(shape, k, scale=scale)
     try:
         np.savez(path, u=rs.user_ids, i=rs.item_ids, r=rs.ratings, nu=rs.num_users,
                  ni=rs.num_items)
@@ -153,7 +154,7 @@ def cpu_share():
     return n, {"host_cpus": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota}
 
 
-def cpu_baseline(shape, k, threads, scale, seed=0, replay=True):
+def cpu_baseline(shape, k, threads, scale, seed=0, replay=True, rs=None):
     """Reference CPU path on a bounded sample of the same workload: the
     MovieLens-shaped generator at ``scale`` of the users, items and draws (so
     per-entity degrees, and with them the CPU's per-rating costs, keep their
@@ -175,7 +176,8 @@ def cpu_baseline(shape, k, threads, scale, seed=0, replay=True):
     share, cpu_info = cpu_share()
     if threads is None:
         threads = share
-    rs = synth.movielens_like(shape, k, scale=scale)
+    if rs is None:
+        rs = synth.movielens_like(shape, k, scale=scale)
     U0, V0 = ref.init_factors(rs.num_users, rs.num_items, k, seed)
     ref.set_thread_count(threads)
     t = {}
@@ -195,6 +197,7 @@ def cpu_baseline(shape, k, threads, scale, seed=0, replay=True):
         from oracle.ref_replay import als_replay
         _, _, _, tr = als_replay(rs.user_ids, rs.item_ids, rs.ratings, k, U0, V0,
                                  max_iteration=3)
+        tr_all = tr
         tr = tr[1:3]          # iterations 2-3: what T(3) - T(1) measures
         cu = sum(x["cg_users"] for x in tr)
         ci = sum(x["cg_items"] for x in tr)
@@ -206,6 +209,7 @@ def cpu_baseline(shape, k, threads, scale, seed=0, replay=True):
             "ms_per_cg_iteration_items": round(ti / max(ci, 1) * 1e3, 3),
             # ratings x CG iterations per second: the trajectory-free rate
             "ratings_cg_iterations_per_s": round(rs.n * (cu + ci) / (tu + ti), 1),
+            "cg_per_iteration": [[x["cg_users"], x["cg_items"]] for x in tr_all],
             "how": ("oracle/ref_replay.als_replay: als() restated around the reference's own "
                     "cg_least_squares_from_python, bit-identical to als_from_python "
                     "(tests/test_oracle.py), iterations 2-3 of the same run")}
@@ -228,14 +232,50 @@ def gpu_cg_rate(st, n_u, n_i):
             "note": "solve phases of the instrumented replay; the Gram is not included"}
 
 
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n):
+    """``--gpus N`` (N > 1) started without a launcher: run this same command
+    under ``torch.distributed.run``, one rank per GPU, as a CHILD process
+    (this process has not touched the GPU: only numpy is loaded), relay the
+    ranks' one JSON line and exit with the launcher's return code.  Replaces
+    the role of the reference's process fan-out
+    (``python/full_data/cluster_server.py:279-305``)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={free_port()}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"[bench] --gpus {n}: launching {' '.join(cmd[1:6])} ...")
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, env=dict(os.environ))
+    lines = [ln for ln in p.stdout.decode(errors="replace").splitlines() if ln.strip()]
+    js = [ln for ln in lines if ln.lstrip().startswith("{") and '"metric"' in ln]
+    for ln in lines:
+        if ln not in js:
+            log(f"[bench] (rank stdout) {ln}")
+    if js:
+        os.write(JSON_FD, (js[-1].strip() + "\n").encode())
+    if p.returncode == 0 and not js:
+        log("[bench] ranks exited 0 without a JSON line")
+        return 1
+    return p.returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--k", type=int, default=64)
     ap.add_argument("--shape", default="ml-full", choices=["ml-full", "ml-100k", "c5"])
-    ap.add_argument("--scale", type=float, default=1.0, help="fraction of the c5 shape")
+    ap.add_argument("--scale", type=float, default=1.0,
+                    help="fraction of the shape (users, items, draws); tests and C5 slices")
     ap.add_argument("--solver", default="cg", choices=["cg", "cholesky"])
     ap.add_argument("--ridge", type=float, default=0.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -249,27 +289,58 @@ def main():
                     help="engine launch-ahead level (include/mr_als.h MR_OPT_CG_SPECULATE)")
     ap.add_argument("--opt", action="append", default=[],
                     help="engine option NAME=VALUE (engine.OPTIONS), repeatable")
-    ap.add_argument("--cpu-scale", type=float, default=0.25)
+    ap.add_argument("--cpu-scale", type=float, default=1.0,
+                    help="fraction of the workload the reference CPU leg runs (1.0: the "
+                         "same data, start and window as the GPU's same_window)")
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="reference threads (default: this process's CPU share)")
+    ap.add_argument("--no-same-window", action="store_true",
+                    help="skip the GPU's iterations-2-3 run from the seed-0 start")
     ap.add_argument("--force-shard", action="store_true",
                     help="use the sharded RCCL path even with one rank (testing)")
     ap.add_argument("--scalars", default="peer", choices=["peer", "collective"],
                     help="sharded runs: CG scalars through the peer all-reduce (IPC-mapped "
                          "buffers; falls back to RCCL if its self-test fails) or RCCL")
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "gloo"],
+                    help="sharded runs: factor all-gather through the native RCCL "
+                         "communicator (one rank per GPU) or, for tests, gloo callbacks "
+                         "(host-staged; lets several ranks share one GPU)")
+    ap.add_argument("--device-map", default=None,
+                    help="test only: comma-separated GPU index per local rank "
+                         "(e.g. 0,0 puts two ranks on GPU 0; needs --comm gloo)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r03.json"),
                     help="per-kernel HBM bytes from a rocprofv3 --pmc run (optional)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        return launch_ranks(args.gpus)
+    world = int(env_world) if env_world is not None else 1
+    if world != args.gpus:
+        log(f"[bench] WORLD_SIZE={world} but --gpus {args.gpus}: refusing to report a "
+            f"{world}-rank run as {args.gpus}")
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    device = local_rank
+    if args.device_map is not None:
+        dm = [int(x) for x in args.device_map.split(",")]
+        if len(dm) <= local_rank:
+            log(f"[bench] --device-map {args.device_map} has no entry for local rank {local_rank}")
+            return 2
+        device = dm[local_rank]
+        if args.comm != "gloo" and len(set(dm[:world])) < min(world, len(dm)):
+            log("[bench] ranks sharing a GPU need --comm gloo (RCCL takes one rank per GPU)")
+            return 2
     dist = None
     if world > 1 or args.force_shard:
         import torch
         import torch.distributed as tdist
-        torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.comm == "gloo":
+            tdist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(device)
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", device))
         dist = tdist
 
     from movie_recommender_amd.engine import AlsContext
@@ -284,7 +355,7 @@ def main():
     else:
         if dist is not None and rank != 0:
             dist.barrier()            # rank 0 generates (or loads) the data first
-        rs = load_data(args.shape, k)
+        rs = load_data(args.shape, k, scale=args.scale)
         if dist is not None and rank == 0:
             dist.barrier()
         n_total, n_users, n_items = rs.n, rs.num_users, rs.num_items
@@ -293,7 +364,7 @@ def main():
 
     t0 = time.perf_counter()
     if c5:
-        from movie_recommender_amd.distributed import attach_rccl, entity_cost, shard_bounds
+        from movie_recommender_amd.distributed import entity_cost, shard_bounds
         if dist is not None:
             ub = shard_bounds(entity_cost(gen.deg, k), world)
             ib = shard_bounds(entity_cost(np.rint(gen.expected_item_counts()).astype(np.int64),
@@ -301,17 +372,18 @@ def main():
             u0, u1, i0, i1 = int(ub[rank]), int(ub[rank + 1]), int(ib[rank]), int(ib[rank + 1])
             uv = gen.user_view(u0, u1)
             iv = gen.item_view(i0, i1)
-            ctx = AlsContext(uv[0], uv[1], uv[2], k, n_users, n_items, device=local_rank,
+            ctx = AlsContext(uv[0], uv[1], uv[2], k, n_users, n_items, device=device,
                              solver=args.solver, ridge=args.ridge, user_range=(u0, u1),
                              item_range=(i0, i1), item_view=iv)
             del uv, iv
-            attach_rccl(ctx, rank, world, ub, ib)
+            from movie_recommender_amd.distributed import TorchComm, attach_comm
+            attach_comm(ctx, TorchComm() if args.comm == "gloo" else "rccl", rank, world, ub, ib)
             if args.scalars == "peer":
                 from movie_recommender_amd.distributed import attach_peer_scalars
                 ctx.peer_scalars = attach_peer_scalars(ctx, rank, world)
         else:
             u, i, r = gen.all_ratings()
-            ctx = AlsContext(u, i, r, k, n_users, n_items, device=local_rank,
+            ctx = AlsContext(u, i, r, k, n_users, n_items, device=device,
                              solver=args.solver, ridge=args.ridge)
             del u, i, r
         ctx.init_factors(0)
@@ -320,12 +392,17 @@ def main():
         U0 = rng.uniform(-1, 1, n_users * (k + 1))
         V0 = rng.uniform(-1, 1, n_items * k)
         if dist is not None:
+            if args.comm == "gloo":
+                from movie_recommender_amd.distributed import TorchComm
+                comm = TorchComm()
+            else:
+                comm = "rccl"
             ctx = sharded_context(rs.user_ids, rs.item_ids, rs.ratings, k, n_users, n_items,
-                                  local_rank, "rccl", solver=args.solver, ridge=args.ridge,
+                                  device, comm, solver=args.solver, ridge=args.ridge,
                                   scalars=args.scalars)
         else:
             ctx = AlsContext(rs.user_ids, rs.item_ids, rs.ratings, k, n_users, n_items,
-                             device=local_rank, solver=args.solver, ridge=args.ridge)
+                             device=device, solver=args.solver, ridge=args.ridge)
         ctx.set_factors(U0, V0)
     if args.no_fuse_start:
         ctx.set_option("fuse_start", 0)
@@ -353,7 +430,8 @@ def main():
         if dist is None:
             return x
         import torch
-        tt = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local_rank}")
+        tt = torch.tensor([x], dtype=torch.float64,
+                          device="cpu" if args.comm == "gloo" else f"cuda:{device}")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         return float(tt.item())
 
@@ -393,6 +471,54 @@ def main():
     elif instrument:
         events_ms = elapsed * 1e3 / args.steps
     ctx.set_timing(False)
+
+    # The reference's window and the trajectory (not c5: its factors are
+    # device-seeded, not the RandomState(0) start the reference uses).
+    # same_window: iterations 2-3 from the seed-0 start -- what the CPU leg's
+    # T(3) - T(1) times -- timed like the main region.
+    # trajectory: CG iterations of every ALS iteration 1 .. warmup + steps
+    # from the same start, one iteration at a time (untimed); its sums over
+    # the timed window must equal the timed region's (the engine is
+    # deterministic), which the line checks.
+    same_window = trajectory = None
+    if not c5 and not args.no_same_window:
+        ctx.set_factors(U0, V0)
+        ctx.iterate(1)
+        barrier()
+        ctx.reset_stats()
+        t = time.perf_counter()
+        ctx.iterate(2)
+        barrier()
+        t_sw = max_over_ranks(time.perf_counter() - t)
+        s2 = ctx.stats()
+        same_window = {"iterations": "2-3 of the RandomState(0) start (T(3) - T(1) of the CPU leg)",
+                       "value": round(n_total * 2 / t_sw, 1), "unit": "ratings/s",
+                       "ms_per_iteration": round(t_sw * 1e3 / 2, 3),
+                       "cg_users": s2["cg_users_total"], "cg_items": s2["cg_items_total"]}
+        ctx.set_factors(U0, V0)
+        trajectory = []
+        for it in range(args.warmup + args.steps):
+            ctx.reset_stats()
+            ctx.iterate(1)
+            s1 = ctx.stats()
+            trajectory.append([s1["cg_users_total"], s1["cg_items_total"]])
+        win = trajectory[args.warmup:]
+        same_window["trajectory_cg_matches"] = (
+            trajectory[1][0] + trajectory[2][0] == same_window["cg_users"]
+            and trajectory[1][1] + trajectory[2][1] == same_window["cg_items"])
+        trajectory = {"cg_per_iteration": trajectory,
+                      "matches_timed_region": (sum(x[0] for x in win) == st["cg_users_total"]
+                                               and sum(x[1] for x in win) == st["cg_items_total"])}
+
+    # per-rank shard sizes (cost-balanced shards are unequal)
+    shards = None
+    if dist is not None:
+        mine = [list(ctx.local_size("users")), list(ctx.local_size("items"))]
+        allr = [None] * world
+        dist.all_gather_object(allr, mine)
+        shards = [{"rank": r, "users": [a[0][0], a[0][0] + a[0][1]], "user_ratings": a[0][2],
+                   "items": [a[1][0], a[1][0] + a[1][1]], "item_ratings": a[1][2]}
+                  for r, a in enumerate(allr)]
 
     # local work units (ratings processed by this rank per iteration)
     n_local_users = ctx.num_ratings
@@ -467,7 +593,7 @@ def main():
                  "half-stars; device-seeded factors)" if c5 else
                  "synthetic (MovieLens-full shape, seeded; no MovieLens data offline)"),
         "config": {"workload": (f"ALS iteration, {args.shape} shape"
-                                + (f" x{args.scale:g}" if c5 and args.scale != 1.0 else "")
+                                + (f" x{args.scale:g}" if args.scale != 1.0 else "")
                                 + f", k={k}, solver={args.solver}"),
                    "k": k, "n_ratings": int(n_total), "users": int(n_users),
                    "items": int(n_items), "solver": args.solver,
@@ -496,14 +622,30 @@ def main():
                    "timed region without per-launch events (no kernel table)"),
         "ms_per_step_with_kernel_events": round(events_ms, 3) if events_ms else None,
         "replay_cg_identical": replay_identical,
+        "same_window": same_window,
+        "trajectory": trajectory,
     }
+    if shards is not None:
+        out["config"]["shards"] = shards
+        out["config"]["comm"] = args.comm
+        if args.device_map is not None:
+            out["config"]["device_map"] = args.device_map
     if rank == 0 and world == 1 and not args.no_cpu and not c5:
         try:
-            cb = cpu_baseline(args.shape, k, args.cpu_threads, args.cpu_scale)
+            cb = cpu_baseline(args.shape, k, args.cpu_threads, args.cpu_scale * args.scale,
+                              rs=rs if args.cpu_scale == 1.0 else None)
         except Exception as e:  # the GPU number stands on its own
             log(f"[bench] cpu baseline failed: {e!r}")
             cb = None
         out["cpu_baseline"] = cb
+        if cb and cb.get("cg") and same_window is not None and args.cpu_scale == 1.0:
+            # same data, start and window on both sides
+            same_window["reference"] = {
+                "value": round(cb["value"], 1),
+                "cg_users": int(round(2 * cb["cg"]["per_als_iteration_users"])),
+                "cg_items": int(round(2 * cb["cg"]["per_als_iteration_items"])),
+                "cores": cb["cores"]}
+            same_window["gpu_over_reference"] = round(same_window["value"] / cb["value"], 1)
     elif rank == 0:
         out["cpu_baseline"] = None
     ctx.close()
@@ -512,6 +654,7 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 # The contract's ONE JSON line goes to the original stdout; everything else a
@@ -523,4 +666,4 @@ if __name__ == "__main__":
     sys.stdout.flush()
     JSON_FD = os.dup(1)
     os.dup2(2, 1)
-    main()
+    sys.exit(main())

@@ -123,13 +123,21 @@ int mr_als_set_rccl(mr_als* ctx, const unsigned char id[128], int rank, int worl
  * runs the single-GPU launch sequence (2 kernels per iteration).  Each rank:
  * mr_als_peer_handle (64 bytes), exchange them (rank order), then
  * mr_als_set_peer with the world x 64 bytes.  Reference scalars:
- * matrix.cpp:485, 497, 507.  A peer that does not arrive within ~30 s fails
- * the solve (< 0) instead of hanging.  mr_als_set_peer with world = 0
- * switches back to the collective scalars.  mr_als_peer_selftest (all ranks
- * together) runs one reduction of {rank + 1, 1} and checks the sums. */
+ * matrix.cpp:485, 497, 507.  A peer that does not arrive within
+ * MR_OPT_PEER_TIMEOUT_S (default 30 s) fails the solve (< 0) instead of
+ * hanging.  mr_als_set_peer runs once per context (a second call is
+ * refused: the exchange buffers' sequence numbers are not reset); with
+ * world = 0 (handles may be NULL) it switches back to the collective scalars
+ * for good.  mr_als_peer_selftest (all ranks together) runs one reduction of
+ * {rank + 1, 1} and checks the sums. */
 int mr_als_peer_handle(mr_als* ctx, unsigned char out[64]);
 int mr_als_set_peer(mr_als* ctx, const unsigned char* handles, int rank, int world);
 int mr_als_peer_selftest(mr_als* ctx);
+/* The user-side Gram's rhs path on the matrix cores needs every weight exact
+ * in bf16 (checked per context on its own ratings).  A sharded run must take
+ * one path on every rank: force < 0 returns this context's flag (0 / 1),
+ * force = 0 clears it (the ranks AND their flags; distributed.py does). */
+int mr_als_weights_bf16(mr_als* ctx, int force);
 /* Latency probe of the peer all-reduce (collective, same iters on every
  * rank): `iters` reductions of one double back to back by one device thread;
  * *us = mean microseconds per reduction (HIP events around the kernel). */
@@ -181,9 +189,13 @@ int mr_als_set_timing(mr_als* ctx, int enable);
  *                         the lines the previous pass left in the Infinity
  *                         Cache); 2 alternates the other way; 0 always
  *                         forwards.  Results are identical in every mode (each
- *                         chunk's partial sums are order-independent terms) */
+ *                         chunk's partial sums are order-independent terms)
+ *   MR_OPT_PEER_TIMEOUT_S device wait for a peer rank's record in the peer
+ *                         all-reduce, seconds (default 30, at most 1e5); on
+ *                         expiry the solve ends with an error (< 0) */
 enum { MR_OPT_FUSE_START = 0, MR_OPT_CG_SPECULATE = 1, MR_OPT_WAIT_TIMEOUT_S = 2,
-       MR_OPT_CG_ONEPASS = 3, MR_OPT_GRAM_RHS_MFMA = 4, MR_OPT_CG_SWEEP = 5 };
+       MR_OPT_CG_ONEPASS = 3, MR_OPT_GRAM_RHS_MFMA = 4, MR_OPT_CG_SWEEP = 5,
+       MR_OPT_PEER_TIMEOUT_S = 6 };
 int mr_als_set_option(mr_als* ctx, int option, double value);
 /* Ratings per Gram work item: heavier entities are split across waves and
  * their partial normal equations combined in order.  Applies to contexts

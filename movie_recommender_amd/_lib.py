@@ -121,6 +121,7 @@ SIGNATURES = {
     "mr_als_peer_handle": (ctypes.c_int, [VP, ctypes.c_void_p]),
     "mr_als_set_peer": (ctypes.c_int, [VP, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "mr_als_peer_selftest": (ctypes.c_int, [VP]),
+    "mr_als_weights_bf16": (ctypes.c_int, [VP, ctypes.c_int]),
     "mr_als_peer_latency": (ctypes.c_int, [VP, ctypes.c_int, DP]),
     "mr_als_destroy": (None, [VP]),
     "mr_als_set_factors": (ctypes.c_int, [VP, DP, DP]),

@@ -224,8 +224,13 @@ int mr_als_peer_handle(mr_als* ctx, unsigned char out[64]) {
 }
 
 int mr_als_set_peer(mr_als* ctx, const unsigned char* handles, int rank, int world) {
-  MR_CHECK(ctx && handles, "null argument");
+  MR_CHECK(ctx && (handles || world == 0), "null argument");
   return guarded([&]() { return ctx->eng.set_peer(handles, rank, world); });
+}
+
+int mr_als_weights_bf16(mr_als* ctx, int force) {
+  MR_CHECK(ctx, "null context");
+  return guarded([&]() { return ctx->eng.weights_bf16(force); });
 }
 
 int mr_als_peer_selftest(mr_als* ctx) {
@@ -298,6 +303,8 @@ int mr_als_set_option(mr_als* ctx, int option, double value) {
       MR_CHECK(value > 0.0, "timeout must be > 0");
       ctx->eng.wait_timeout_s = value;
       return 0;
+    case MR_OPT_PEER_TIMEOUT_S:
+      return guarded([&]() { return ctx->eng.set_peer_timeout(value); });
     default: MR_CHECK(false, "unknown option");
   }
 }

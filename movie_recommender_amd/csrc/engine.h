@@ -92,6 +92,7 @@ struct Engine {
                             // decided on exact published states, so every rank
                             // of a sharded run issues the same launches)
   double wait_timeout_s = 300.0;   // host wait for a published CG state
+  double peer_timeout_s = 30.0;    // device wait for a peer's record (peer all-reduce)
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
   std::vector<Pending> pending;
@@ -110,6 +111,7 @@ struct Engine {
   PeerComm* d_peer = nullptr;
   std::vector<void*> peer_opened;        // peers' buffers mapped by IPC
   bool peer_on = false;
+  bool peer_used = false;                // set_peer ran (it runs once per context)
 
   ~Engine();
   int init(int dev, int k, int64_t U, int64_t I, int64_t n_u, const int* uv_uid,
@@ -130,6 +132,8 @@ struct Engine {
   int set_rccl(const unsigned char* id, int rank, int world);
   int peer_handle(unsigned char* out64);
   int set_peer(const unsigned char* handles, int rank, int world);
+  int set_peer_timeout(double seconds);
+  int weights_bf16(int force);
   int peer_selftest();
   int peer_latency(int iters, double* us);
   // padded all-gather staging (both transports): every shard padded to the

@@ -551,6 +551,12 @@ int Engine::peer_handle(unsigned char* out64) {
 // sequence (matvec, update) with no collective launch in between.  All
 // ranks must call this (after exchanging the handles of peer_handle) before
 // their next solve; the factor all-gather keeps its transport.
+//
+// Once only: the exchange buffers' sequence numbers start at 0 with the first
+// mapping, so a second set_peer (stale tags of the earlier setup still in the
+// peers' buffers could satisfy a new reduction) is refused; world == 0
+// switches back to the collective scalars for good (the mappings stay open
+// until the context is destroyed).
 int Engine::set_peer(const unsigned char* handles, int rank, int world) {
   if (world == 0) {   // back to the collective scalars (e.g. a failed self-test)
     MR_HIP(hipSetDevice(device));
@@ -558,15 +564,19 @@ int Engine::set_peer(const unsigned char* handles, int rank, int world) {
     MR_H2D((char*)d_state + offsetof(CgState, peer), &none, sizeof(none), stream);
     MR_HIP(hipStreamSynchronize(stream));
     peer_on = false;
+    peer_used = true;
     return 0;
   }
   MR_CHECK(handles, "null handles");
   MR_CHECK(world >= 1 && world <= kMaxPeers && rank >= 0 && rank < world, "bad rank/world");
   MR_CHECK(peer_buf, "mr_als_peer_handle must be called first");
+  MR_CHECK(!peer_used, "the peer all-reduce is set up once per context");
   MR_HIP(hipSetDevice(device));
+  peer_used = true;
   PeerComm pc{};
   pc.world = world;
   pc.rank = rank;
+  pc.timeout_ticks = (uint64_t)(peer_timeout_s * 1e8);
   for (int q = 0; q < world; ++q) {
     if (q == rank) {
       pc.buf[q] = peer_buf;
@@ -586,6 +596,32 @@ int Engine::set_peer(const unsigned char* handles, int rank, int world) {
   MR_HIP(hipStreamSynchronize(stream));
   peer_on = true;
   return 0;
+}
+
+// Device wait for a peer's record, seconds (MR_OPT_PEER_TIMEOUT_S); takes
+// effect at once when the peer all-reduce is already mapped.
+int Engine::set_peer_timeout(double seconds) {
+  MR_CHECK(seconds > 0.0 && seconds <= 1e5, "peer timeout must be in (0, 1e5] s");
+  peer_timeout_s = seconds;
+  if (d_peer) {
+    MR_HIP(hipSetDevice(device));
+    const uint64_t ticks = (uint64_t)(seconds * 1e8);
+    MR_H2D((char*)d_peer + offsetof(PeerComm, timeout_ticks), &ticks, sizeof(ticks), stream);
+    MR_HIP(hipStreamSynchronize(stream));
+  }
+  return 0;
+}
+
+// The user-side Gram's rhs path (W block on the matrix cores) needs every
+// weight exact in bf16; a sharded run must take the same path on every rank
+// (the paths round differently), so the ranks agree on the flag:
+// force < 0 reads it, force == 0 clears it (force == 1 is rejected unless
+// this rank's ratings allow it).
+int Engine::weights_bf16(int force) {
+  if (force < 0) return w_bf16 ? 1 : 0;
+  MR_CHECK(force == 0 || w_bf16, "this rank's ratings are not exact in bf16");
+  w_bf16 = force != 0;
+  return w_bf16 ? 1 : 0;
 }
 
 // One reduction of {rank + 1, 1} through the mapped buffers (collective: all

@@ -192,12 +192,19 @@ __device__ __forceinline__ int64_t xsum_collect(int64_t* __restrict__ bins, int 
   int64_t t = 0;
   if (lane < NV * kXW) {
     const int v = lane / kXW, d = lane % kXW;
+    // all bin loads in flight at once, then the (exact, order-free) sum,
+    // then the clears: a load-add-clear per bin put 16 dependent memory
+    // round trips into the serial tail of every CG iteration (~8 us)
+    int64_t* a = bins + (int64_t)v * kXW + d;
+    int64_t x[kXBins];
 #pragma unroll
-    for (int b = 0; b < kXBins; ++b) {
-      int64_t* a = bins + ((int64_t)b * NV + v) * kXW + d;
-      t += __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(a, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    for (int b = 0; b < kXBins; ++b)
+      x[b] = __hip_atomic_load(a + (int64_t)b * NV * kXW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int b = 0; b < kXBins; ++b) t += x[b];
+#pragma unroll
+    for (int b = 0; b < kXBins; ++b)
+      __hip_atomic_store(a + (int64_t)b * NV * kXW, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   return t;
 }
@@ -599,7 +606,9 @@ __device__ __forceinline__ void acc_matvec(const floatx4 (&acc)[NB * (NB + 1) / 
         R[r] = fma(use_r ? a : 0.0, vj, R[r]);
         cc[bj] = fma(use_c ? a : 0.0, vr[r], cc[bj]);
       }
+#ifdef MR_ACC_SB   // per-tile scheduling barrier (off: Gram users / items -1 %)
       __builtin_amdgcn_sched_barrier(0);
+#endif
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) sc.partR[4 * bi + r][lane] = R[r];
@@ -1818,8 +1827,9 @@ __device__ __forceinline__ void apply_beta(CgScalars& v, double rr2) {
 // protocol), so sequence numbers agree; a slot is reused only after every
 // rank has passed kPeerSlots - 1 later reductions, each of which needed this
 // rank's data, so no record is overwritten before it is read.  A peer that
-// does not arrive within ~30 s sets `error` and the caller ends the solve
-// with ret = -1 (the host reports it) instead of spinning forever.
+// does not arrive within pc->timeout_ticks (MR_OPT_PEER_TIMEOUT_S, default
+// 30 s) sets `error` and the caller ends the solve with ret = -1 (the host
+// reports it) instead of spinning forever.
 // Returns false on timeout.
 __device__ bool peer_sum(PeerComm* pc, double* vals, int count) {
   const uint32_t s = pc->seq + 1;
@@ -1839,7 +1849,7 @@ __device__ bool peer_sum(PeerComm* pc, double* vals, int count) {
     const double* rec = pc->buf[rank] + (slot * world + q) * kPeerRec;
     while (__hip_atomic_load(reinterpret_cast<const uint64_t*>(rec + kPeerRec - 1), __ATOMIC_ACQUIRE,
                              __HIP_MEMORY_SCOPE_SYSTEM) != (uint64_t)s) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 3000000000ull) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > pc->timeout_ticks) {
         pc->error = 1;
         return false;
       }
@@ -1888,7 +1898,7 @@ __device__ bool peer_sum_lanes(PeerComm* pc, int64_t& val, int count) {
       const int64_t* rec = reinterpret_cast<const int64_t*>(pc->buf[rank]) + (slot * world + q) * kPeerRec;
       while (__hip_atomic_load(reinterpret_cast<const uint64_t*>(rec + kPeerRec - 1),
                                __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != (uint64_t)s) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 3000000000ull) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > pc->timeout_ticks) {
           pc->error = 1;
           ok = 0;
           break;

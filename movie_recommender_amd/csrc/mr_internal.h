@@ -190,6 +190,8 @@ struct PeerComm {
   int32_t world, rank;
   uint32_t seq;            // reductions done (advanced by the reducing thread)
   int32_t error;           // 1: a peer did not arrive within the timeout
+  uint64_t timeout_ticks;  // give up on a peer after this many s_memrealtime
+                           // ticks (100 MHz; MR_OPT_PEER_TIMEOUT_S)
   double* buf[kMaxPeers];  // rank q's exchange buffer, mapped into this process
 };
 

@@ -139,6 +139,38 @@ class TorchComm:
             return -1
 
 
+def agree_rhs_path(ctx):
+    """Every rank takes the same user-side Gram rhs path: the matrix-core
+    rhs needs every weight exact in bf16, which each context checks on its
+    own ratings (``mr_als_weights_bf16``); the ranks AND their flags so that
+    no rank takes a path that rounds differently from the others'.
+    Collective."""
+    import torch
+    import torch.distributed as dist
+    L = _lib.lib()
+    mine = _lib.check(L.mr_als_weights_bf16(ctx._h, -1), "mr_als_weights_bf16")
+    flag = torch.tensor([mine], dtype=torch.int32)
+    if dist.get_backend() == "nccl":
+        flag = flag.cuda()
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) == 0 and mine:
+        _lib.check(L.mr_als_weights_bf16(ctx._h, 0), "mr_als_weights_bf16")
+    return int(flag.item()) == 1
+
+
+def attach_comm(ctx, comm, rank, world, user_begin, item_begin):
+    """Attach this rank's factor all-gather transport: ``comm="rccl"`` (the
+    native RCCL communicator) or a ``TorchComm`` (host-staged callbacks over
+    any torch.distributed backend), then agree on the rhs path.
+    Collective."""
+    if comm == "rccl":
+        attach_rccl(ctx, rank, world, user_begin, item_begin)
+    else:
+        ctx.set_comm(comm.struct, user_begin, item_begin)
+        ctx._comm_owner = comm
+    agree_rhs_path(ctx)
+
+
 def attach_rccl(ctx, rank, world, user_begin, item_begin):
     """Give ``ctx`` a native RCCL communicator: rank 0 draws the unique id,
     ``torch.distributed`` (any backend) broadcasts its 128 bytes, then every
@@ -160,14 +192,17 @@ def attach_rccl(ctx, rank, world, user_begin, item_begin):
     ctx._rccl = (ub, ib)
 
 
-def attach_peer_scalars(ctx, rank, world):
+def attach_peer_scalars(ctx, rank, world, _fail_set_peer=False):
     """Switch ``ctx``'s CG scalars to the peer all-reduce (include/mr_als.h
     ``mr_als_set_peer``): every rank exports its exchange buffer's IPC handle,
     ``torch.distributed`` gathers the handles in rank order, every rank maps
     its peers', and one self-test reduction checks the sums.  Collective: all
     ranks call it.  Returns True on success; on any rank's failure every rank
     keeps its collective scalars (each step's outcome is agreed by an
-    all-reduce)."""
+    all-reduce, and a rank whose own step succeeded switches back with
+    ``mr_als_set_peer(world=0)``; a failure of that reset raises).
+    ``_fail_set_peer`` (tests only) makes this rank's ``mr_als_set_peer``
+    fail (an out-of-range world)."""
     import torch
     import torch.distributed as dist
     L = _lib.lib()
@@ -186,13 +221,16 @@ def attach_peer_scalars(ctx, rank, world):
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         return int(flag.item()) == 1
 
-    if not agree(L.mr_als_set_peer(ctx._h, joined, int(rank), int(world)) == 0):
-        L.mr_als_set_peer(ctx._h, None, int(rank), 0)
+    def reset():
+        _lib.check(L.mr_als_set_peer(ctx._h, None, int(rank), 0), "mr_als_set_peer(world=0)")
         return False
+
+    w_arg = 1 << 20 if _fail_set_peer else int(world)
+    if not agree(L.mr_als_set_peer(ctx._h, joined, int(rank), w_arg) == 0):
+        return reset()
     # one reduction through the mapped buffers on every rank before trusting them
     if not agree(L.mr_als_peer_selftest(ctx._h) == 0):
-        L.mr_als_set_peer(ctx._h, None, int(rank), 0)
-        return False
+        return reset()
     ctx._peer = joined
     return True
 
@@ -210,12 +248,10 @@ def sharded_context(user_ids, item_ids, ratings, k, num_users, num_items, device
     rank, world = dist.get_rank(), dist.get_world_size()
     (u0, u1), (i0, i1), uv, iv, ub, ib = shard_views(
         user_ids, item_ids, ratings, num_users, num_items, rank, world, k=k, bounds=bounds)
+    fail_peer = kw.pop("_fail_set_peer", False)
     ctx = AlsContext(uv[0], uv[1], uv[2], k, num_users, num_items, device=device,
                      user_range=(u0, u1), item_range=(i0, i1), item_view=iv, **kw)
-    if comm == "rccl":
-        attach_rccl(ctx, rank, world, ub, ib)
-    else:
-        ctx.set_comm(comm.struct, ub, ib)
-        ctx._comm_owner = comm
-    ctx.peer_scalars = scalars == "peer" and attach_peer_scalars(ctx, rank, world)
+    attach_comm(ctx, comm, rank, world, ub, ib)
+    ctx.peer_scalars = scalars == "peer" and attach_peer_scalars(ctx, rank, world,
+                                                                 _fail_set_peer=fail_peer)
     return ctx

@@ -27,10 +27,11 @@ from . import ref
 
 
 def als_replay(user_ids, item_ids, ratings, k, U0, V0, min_r_decrease=0.01,
-               max_iteration=200):
+               max_iteration=200, on_iteration=None):
     """Returns ``(U, V, ret, trace)``; ``trace`` has one dict per ALS
     iteration: ``cg_users``, ``cg_items`` (iterations), ``t_users``,
-    ``t_items`` (seconds inside the reference CG), ``rr``."""
+    ``t_items`` (seconds inside the reference CG), ``rr``.
+    ``on_iteration(it, record)`` is called after each iteration (progress)."""
     uid = np.ascontiguousarray(user_ids, np.int32)
     iid = np.ascontiguousarray(item_ids, np.int32)
     r = np.ascontiguousarray(ratings, np.float64)
@@ -67,6 +68,8 @@ def als_replay(user_ids, item_ids, ratings, k, U0, V0, min_r_decrease=0.01,
         t_i = time.perf_counter() - t0
         V[:] = x
         trace.append(dict(cg_users=cu, cg_items=ci, t_users=t_u, t_items=t_i, rr=rr))
+        if on_iteration is not None:
+            on_iteration(it, trace[-1])
         if it >= 3 and (old_rr - rr) / old_rr < min_r_decrease:
             return U, V, it, trace
         va_u[:, :k] = Vm[iid]                          # fill_user_A (refresh)

@@ -14,6 +14,14 @@ Modes
   engine_rccl  the HIP engine with its native RCCL communicator.
   engine_peer  engine_gloo with the CG scalars through the peer all-reduce
                (IPC-mapped exchange buffers, include/mr_als.h mr_als_set_peer).
+  peer_fail_setup   engine_peer whose last rank's mr_als_set_peer fails: every
+               rank must fall back to the collective scalars (peer_scalars
+               False, the self-test refused as "not set up") and the run must
+               still complete on them.
+  peer_missing_rank engine_peer with MR_OPT_PEER_TIMEOUT_S = 3; the last rank
+               never starts its solve: rank 0's run must fail (RuntimeError,
+               ret -1 from the engine) within the bound instead of hanging;
+               rank 0 saves the elapsed seconds and the message.
 """
 import argparse
 import os
@@ -119,6 +127,57 @@ def engine_sharded(d, max_iteration, rank, world, mode, skew=False, onepass=1):
     return U, V, ret
 
 
+def peer_fail_setup(d, max_iteration, rank, world):
+    import torch.distributed as dist
+    from movie_recommender_amd import _lib
+    from movie_recommender_amd.distributed import TorchComm, sharded_context
+    from movie_recommender_amd.engine import device_count
+    k, nU, nI = int(d["k"]), int(d["num_users"]), int(d["num_items"])
+    dev = rank % max(1, device_count())
+    ctx = sharded_context(d["user_ids"], d["item_ids"], d["ratings"], k, nU, nI, dev,
+                          TorchComm(), scalars="peer", _fail_set_peer=(rank == world - 1))
+    assert not ctx.peer_scalars, "a rank kept the peer scalars after another rank failed"
+    assert _lib.lib().mr_als_peer_selftest(ctx._h) < 0, "peer_on still set after the fallback"
+    assert "not set up" in _lib.last_error(), _lib.last_error()
+    ctx.set_factors(d["U0"], d["V0"])
+    ret = ctx.run(0.01, max_iteration)
+    U, V = ctx.get_factors()
+    ctx.close()
+    dist.barrier()
+    return U, V, ret
+
+
+def peer_missing_rank(d, rank, world, out):
+    import time
+    import torch.distributed as dist
+    from movie_recommender_amd.distributed import TorchComm, sharded_context
+    from movie_recommender_amd.engine import device_count
+    k, nU, nI = int(d["k"]), int(d["num_users"]), int(d["num_items"])
+    dev = rank % max(1, device_count())
+    ctx = sharded_context(d["user_ids"], d["item_ids"], d["ratings"], k, nU, nI, dev,
+                          TorchComm(), scalars="peer")
+    assert ctx.peer_scalars, "peer all-reduce was not set up"
+    ctx.set_option("peer_timeout_s", 3.0)
+    ctx.set_factors(d["U0"], d["V0"])
+    dist.barrier()
+    if rank == world - 1:
+        # the missing rank: never enters the solve; waits for rank 0's verdict
+        dist.barrier()
+        ctx.close()
+        return
+    t0 = time.perf_counter()
+    msg = ""
+    try:
+        ctx.run(0.01, 3)
+    except RuntimeError as e:
+        msg = str(e)
+    el = time.perf_counter() - t0
+    if rank == 0:
+        np.savez(out, elapsed=el, msg=np.array(msg))
+    dist.barrier()
+    ctx.close()
+
+
 def comm_padded(rank, world):
     """The callback transport's host side as the engine drives it: the padded
     exchange table (world x maxrows rows, this rank's packed block at
@@ -158,9 +217,16 @@ def main():
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     d = load(a.fixture)
+    if a.mode == "peer_missing_rank":
+        peer_missing_rank(d, rank, world, a.out)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     if a.mode == "comm_padded":
         U, V = comm_padded(rank, world)
         ret = world
+    elif a.mode == "peer_fail_setup":
+        U, V, ret = peer_fail_setup(d, a.max_iteration, rank, world)
     elif a.mode == "oracle":
         U, V, ret = oracle_sharded(d, a.max_iteration, rank, world)
     else:

@@ -325,3 +325,36 @@ def test_engine_peer_scalars_match_collective(gpu, tmp_path, fixture, max_it, np
             Us, Vs = ctx.get_factors()
         assert ret_s == ret1
         assert np.array_equal(Us, U1) and np.array_equal(Vs, V1), (rel_err(U1, Us), rel_err(V1, Vs))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nproc", [2, 3])
+def test_peer_setup_failure_falls_back_on_every_rank(gpu, tmp_path, nproc):
+    """one rank's mr_als_set_peer fails -> every rank (including
+    those whose own set_peer succeeded) switches back to the collective
+    scalars, so all ranks issue the same launches; the run completes on the
+    collective path and matches the compiled reference's golden."""
+    fixture = "als_dense_300x260_k64.npz"
+    d = load_golden(fixture)
+    U, V, ret = run_workers("peer_fail_setup", fixture, nproc, tmp_path, 200)
+    assert ret == int(d["ret"])
+    assert rel_err(U, d["U"]) < 1e-5 and rel_err(V, d["V"]) < 1e-5
+
+
+@pytest.mark.gpu
+def test_peer_missing_rank_fails_within_timeout(gpu, tmp_path):
+    """A rank that never arrives: the peer all-reduce gives up after
+    MR_OPT_PEER_TIMEOUT_S (3 s here) and the solve fails with an error the
+    Python layer raises -- bounded, no hang (the process exits normally)."""
+    fixture = "als_dense_300x260_k64.npz"
+    out = str(tmp_path / "missing.npz")
+    env = dict(os.environ, OMP_NUM_THREADS="2", MR_QUIET="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", WORKER, "--mode",
+           "peer_missing_rank", "--fixture", fixture, "--out", out]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    with np.load(out) as z:
+        el, msg = float(z["elapsed"]), str(z["msg"])
+    assert "timed out" in msg, msg
+    assert 2.5 < el < 30.0, el
