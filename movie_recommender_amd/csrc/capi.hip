@@ -32,14 +32,18 @@ int env_device() {
 
 template <typename F>
 int guarded(F&& f) {
+  int rc = -1;
   try {
-    return f();
+    rc = f();
   } catch (const std::bad_alloc&) {
     mr::set_error("host out of memory");
   } catch (...) {
     mr::set_error("unexpected C++ exception");
   }
-  return -1;
+  // a launch helper that failed inside a timed interval leaves its event pair
+  // in this thread's launch-timing slot: never carry it into the next call
+  if (rc < 0) mr::t_launch = mr::LaunchTiming{};
+  return rc;
 }
 // Device scratch of the test hooks (freed with its stream).
 struct DevScratch {
@@ -491,22 +495,28 @@ int mr_test_unstage_rows(int device, int world, int skip, const long long* rb, l
     MR_HIP(hipSetDevice(device));
     DevScratch d;
     MR_HIP(hipStreamCreateWithFlags(&d.s, hipStreamNonBlocking));
-    float *dfac, *dbias = nullptr, *drecv, *drecv_b = nullptr;
+    // the gathered layout: one block per rank, factors then the padded bias
+    const int64_t per = mr::ag_block_floats(maxrows, ldk, bias != nullptr);
+    std::vector<float> packed((size_t)world * per, 0.f);
+    for (int r = 0; r < world; ++r) {
+      memcpy(packed.data() + (size_t)r * per, recv + (size_t)r * maxrows * ldk,
+             (size_t)maxrows * ldk * 4);
+      if (bias)
+        memcpy(packed.data() + (size_t)r * per + maxrows * ldk, recv_b + (size_t)r * maxrows,
+               (size_t)maxrows * 4);
+    }
+    float *dfac, *dbias = nullptr, *drecv;
     int64_t* drb;
-    if (d.alloc(&dfac, rows * ldk) || d.alloc(&drecv, (int64_t)world * maxrows * ldk) ||
+    if (d.alloc(&dfac, rows * ldk) || d.alloc(&drecv, (int64_t)world * per) ||
         d.alloc(&drb, world + 1))
       return -1;
-    if (bias && (d.alloc(&dbias, rows) || d.alloc(&drecv_b, (int64_t)world * maxrows))) return -1;
+    if (bias && d.alloc(&dbias, rows)) return -1;
     std::vector<int64_t> rb64(rb, rb + world + 1);
     MR_H2D(drb, rb64.data(), (world + 1) * 8, d.s);
     MR_H2D(dfac, fac, rows * ldk * 4, d.s);
-    MR_H2D(drecv, recv, (int64_t)world * maxrows * ldk * 4, d.s);
-    if (bias) {
-      MR_H2D(dbias, bias, rows * 4, d.s);
-      MR_H2D(drecv_b, recv_b, (int64_t)world * maxrows * 4, d.s);
-    }
-    if (mr::launch_unstage_rows(d.s, world, skip, drb, maxrows, ldk, drecv, drecv_b, dfac,
-                                dbias))
+    MR_H2D(drecv, packed.data(), (int64_t)world * per * 4, d.s);
+    if (bias) MR_H2D(dbias, bias, rows * 4, d.s);
+    if (mr::launch_unstage_rows(d.s, world, skip, drb, maxrows, ldk, drecv, dfac, dbias))
       return -1;
     MR_D2H(fac, dfac, rows * ldk * 4, d.s);
     if (bias) MR_D2H(bias, dbias, rows * 4, d.s);

@@ -123,6 +123,7 @@ struct CgLs {
     MR_CHECK(rows_ >= 0 && cols_ >= 0, "negative matrix dimension");
     MR_CHECK(hrp && hrp[0] == 0, "row indices must start at 0");
     for (int i = 0; i < rows_; ++i) MR_CHECK(hrp[i + 1] >= hrp[i], "row indices not monotone");
+    MR_CHECK((hci && hv) || hrp[rows_] == 0, "null column indices or values");
     device = dev;
     rows = rows_;
     cols = cols_;
@@ -225,6 +226,7 @@ struct CgLs {
   }
 
   int solve(const double* hb, double* hx, double min_dec, int max_it, double* final_rr) {
+    MR_CHECK((hb || rows == 0) && (hx || cols == 0), "null b or x");
     MR_HIP(hipSetDevice(device));
     if (rows) {
       MR_H2D(b_in, hb, rows * 8, s);
@@ -344,7 +346,13 @@ void mr_cg_destroy(mr_cg* ctx) { delete ctx; }
 int mr_cg_solve(mr_cg* ctx, const double* b, double* x, double min_r_decrease, int max_iteration,
                 double* final_rr) {
   MR_CHECK(ctx, "null context");
-  return cg_guarded([&]() { return ctx->c.solve(b, x, min_r_decrease, max_iteration, final_rr); });
+  const int rc =
+      cg_guarded([&]() { return ctx->c.solve(b, x, min_r_decrease, max_iteration, final_rr); });
+  // a launch helper that failed inside a timed interval left its event pair
+  // in this thread's launch-timing slot: drop it, so that the next launch on
+  // the thread (any context) does not record into this context's events
+  mr::t_launch = mr::LaunchTiming{};
+  return rc;
 }
 
 int mr_cg_set_timing(mr_cg* ctx, int enable) {

@@ -37,8 +37,8 @@ struct Side {
 // All-gather staging of one factor table (sharded runs, RCCL).
 struct AgStage {
   int64_t maxrows = 0;                  // rows of the largest shard
-  float *send = nullptr, *recv = nullptr;       // maxrows x ldk, world x maxrows x ldk
-  float *send_b = nullptr, *recv_b = nullptr;   // user bias column
+  int64_t per = 0;                      // floats per rank block (ag_block_floats)
+  float *send = nullptr, *recv = nullptr;       // one block, world blocks
   int64_t* rb = nullptr;                // device copy of the world+1 row boundaries
 };
 

@@ -72,8 +72,7 @@ Engine::~Engine() {
     free_side(si, stream);
     dfree(Ufac, stream); dfree(Ubias, stream); dfree(Vfac, stream);
     for (AgStage* A : {&ag_u, &ag_i}) {
-      dfree(A->send, stream); dfree(A->recv, stream); dfree(A->send_b, stream);
-      dfree(A->recv_b, stream); dfree(A->rb, stream);
+      dfree(A->send, stream); dfree(A->recv, stream); dfree(A->rb, stream);
     }
     dfree(d_state, stream); dfree(partials, stream); dfree(d_flag, stream); dfree(xbins, stream);
     dfree(d_peer, stream);
@@ -689,14 +688,11 @@ int Engine::alloc_ag(int world) {
       mx = std::max(mx, rb[r + 1] - rb[r]);
     }
     AgStage& A = side == 0 ? ag_u : ag_i;
-    dfree(A.send, stream); dfree(A.recv, stream); dfree(A.send_b, stream);
-    dfree(A.recv_b, stream); dfree(A.rb, stream);
+    dfree(A.send, stream); dfree(A.recv, stream); dfree(A.rb, stream);
     A.maxrows = mx;
-    if (dalloc(&A.send, mx * ldk, stream) || dalloc(&A.recv, (int64_t)world * mx * ldk, stream) ||
+    A.per = ag_block_floats(mx, ldk, side == 0);
+    if (dalloc(&A.send, A.per, stream) || dalloc(&A.recv, (int64_t)world * A.per, stream) ||
         dalloc(&A.rb, world + 1, stream))
-      return -1;
-    if (side == 0 &&
-        (dalloc(&A.send_b, mx, stream) || dalloc(&A.recv_b, (int64_t)world * mx, stream)))
       return -1;
     std::vector<int64_t> rb64(rb.begin(), rb.end());
     MR_H2D(A.rb, rb64.data(), rb64.size() * 8, stream);
@@ -728,8 +724,9 @@ int Engine::allreduce_state_slot(int count) {
 
 // Replicate the freshly solved shard rows of a factor table on every rank:
 // the own rows are packed into a send buffer, exchanged as ONE all-gather of
-// equal, padded shards (world x maxrows rows), and every other rank's rows
-// unstaged into place by one kernel (users: the bias column likewise).  The
+// equal, padded shards (world x maxrows rows; users: the bias column rides in
+// the same block), and every other rank's rows unstaged into place by one
+// kernel.  The
 // device side (pack_rows -> padded buffers -> unstage_rows) is the same for
 // both transports: RCCL gathers the device buffers directly; the callback
 // transport carries the same padded buffers through host memory and
@@ -744,35 +741,22 @@ int Engine::allgather_side(bool user) {
   float* fac = user ? Ufac : Vfac;
   float* bias = user ? Ubias : nullptr;
   if (launch_pack_rows(stream, rb[rank], rb[rank + 1] - rb[rank], ldk, fac, bias, A.send,
-                       A.send_b))
+                       bias ? A.send + A.maxrows * ldk : nullptr))
     return -1;
   if (rccl) {
-    MR_NCCL(ncclGroupStart());
-    MR_NCCL(ncclAllGather(A.send, A.recv, (size_t)(A.maxrows * ldk), ncclFloat,
-                          (ncclComm_t)rccl, stream));
-    if (user)
-      MR_NCCL(ncclAllGather(A.send_b, A.recv_b, (size_t)A.maxrows, ncclFloat, (ncclComm_t)rccl,
-                            stream));
-    MR_NCCL(ncclGroupEnd());
+    MR_NCCL(ncclAllGather(A.send, A.recv, (size_t)A.per, ncclFloat, (ncclComm_t)rccl, stream));
   } else {
-    const int64_t per = A.maxrows * ldk;
-    h_ag.resize((size_t)world * per + (user ? (size_t)world * A.maxrows : 0));
+    // the callback carries each rank's block as one padded "row" of A.per floats
+    h_ag.resize((size_t)world * A.per);
     float* tab = h_ag.data();
-    float* tab_b = tab + (size_t)world * per;
-    MR_D2H(tab + (size_t)rank * per, A.send, per * 4, stream);
-    if (user) MR_D2H(tab_b + (size_t)rank * A.maxrows, A.send_b, A.maxrows * 4, stream);
+    MR_D2H(tab + (size_t)rank * A.per, A.send, A.per * 4, stream);
     std::vector<long long> prb(world + 1);
-    for (int r = 0; r <= world; ++r) prb[r] = (long long)r * A.maxrows;
-    MR_CHECK(comm.allgather_rows(comm.user, tab, ldk, prb.data(), world) == 0,
+    for (int r = 0; r <= world; ++r) prb[r] = r;
+    MR_CHECK(comm.allgather_rows(comm.user, tab, (int)A.per, prb.data(), world) == 0,
              "allgather callback failed");
-    if (user)
-      MR_CHECK(comm.allgather_rows(comm.user, tab_b, 1, prb.data(), world) == 0,
-               "allgather callback failed");
-    MR_H2D(A.recv, tab, (size_t)world * per * 4, stream);
-    if (user) MR_H2D(A.recv_b, tab_b, (size_t)world * A.maxrows * 4, stream);
+    MR_H2D(A.recv, tab, (size_t)world * A.per * 4, stream);
   }
-  return launch_unstage_rows(stream, world, rank, A.rb, A.maxrows, ldk, A.recv, A.recv_b, fac,
-                             bias);
+  return launch_unstage_rows(stream, world, rank, A.rb, A.maxrows, ldk, A.recv, fac, bias);
 }
 
 // Sharded CG: all-reduce the slot the last block filled, then apply the rule.

@@ -3147,9 +3147,12 @@ int launch_pack_rows(hipStream_t s, int64_t r0, int64_t n, int ldk, const float*
   return 0;
 }
 
+// The gathered buffer holds one block per rank: maxrows x ldk factor floats,
+// then (users) maxrows bias floats padded to a multiple of 4 (ag_block_floats),
+// so factors and biases travel in ONE all-gather.
 __global__ void unstage_rows_kernel(int world, int skip, const int64_t* __restrict__ rb,
-                                    int64_t maxrows, int ldk4, const float4* __restrict__ recv,
-                                    const float* __restrict__ recv_b, float4* __restrict__ fac,
+                                    int64_t maxrows, int ldk4, int64_t stride4,
+                                    const float4* __restrict__ recv, float4* __restrict__ fac,
                                     float* __restrict__ bias) {
   const int64_t per = maxrows * ldk4;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < (int64_t)world * per;
@@ -3159,17 +3162,22 @@ __global__ void unstage_rows_kernel(int world, int skip, const int64_t* __restri
     const int64_t j = rem / ldk4;
     if (r == skip || j >= rb[r + 1] - rb[r]) continue;
     const int c = (int)(rem - j * ldk4);
-    fac[(rb[r] + j) * ldk4 + c] = recv[t];
-    if (bias && c == 0) bias[rb[r] + j] = recv_b[(int64_t)r * maxrows + j];
+    fac[(rb[r] + j) * ldk4 + c] = recv[r * stride4 + rem];
+    if (bias && c == 0)
+      bias[rb[r] + j] = reinterpret_cast<const float*>(recv + r * stride4 + per)[j];
   }
 }
 
+int64_t ag_block_floats(int64_t maxrows, int ldk, bool with_bias) {
+  return maxrows * ldk + (with_bias ? (maxrows + 3) / 4 * 4 : 0);
+}
+
 int launch_unstage_rows(hipStream_t s, int world, int skip, const int64_t* rb,
-                        int64_t maxrows, int ldk, const float* recv, const float* recv_b,
-                        float* fac, float* bias) {
+                        int64_t maxrows, int ldk, const float* recv, float* fac, float* bias) {
   const int ldk4 = ldk / 4;
+  const int64_t stride4 = ag_block_floats(maxrows, ldk, bias != nullptr) / 4;
   unstage_rows_kernel<<<grid_for((int64_t)world * maxrows * ldk4), 256, 0, s>>>(
-      world, skip, rb, maxrows, ldk4, reinterpret_cast<const float4*>(recv), recv_b,
+      world, skip, rb, maxrows, ldk4, stride4, reinterpret_cast<const float4*>(recv),
       reinterpret_cast<float4*>(fac), bias);
   MR_HIP(hipGetLastError());
   return 0;

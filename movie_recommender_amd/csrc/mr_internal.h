@@ -334,13 +334,15 @@ int launch_unpack_factors(hipStream_t s, int64_t rows, int width, int k,
 int launch_pack_factors(hipStream_t s, int64_t rows, int width, int k, int ldk,
                         const float* fac, const float* bias, double* dst);
 // Sharded all-gather staging: pack rows [r0, r0+n) of fac (and bias) into
-// send; unstage world x maxrows gathered rows into their table rows
-// (rb[s] .. rb[s+1]) for every rank s != skip.
+// send (bias at send_b); unstage the world gathered blocks -- each
+// ag_block_floats(maxrows, ldk, bias != null) floats: maxrows x ldk factors,
+// then the bias column padded to 4 -- into their table rows (rb[s] ..
+// rb[s+1]) for every rank s != skip.
+int64_t ag_block_floats(int64_t maxrows, int ldk, bool with_bias);
 int launch_pack_rows(hipStream_t s, int64_t r0, int64_t n, int ldk, const float* fac,
                      const float* bias, float* send, float* send_b);
 int launch_unstage_rows(hipStream_t s, int world, int skip, const int64_t* rb,
-                        int64_t maxrows, int ldk, const float* recv, const float* recv_b,
-                        float* fac, float* bias);
+                        int64_t maxrows, int ldk, const float* recv, float* fac, float* bias);
 // Seeded uniform(-1, 1) factor table on the device (table 0: U with bias,
 // 1: V); the same values on every rank.
 int launch_init_factors(hipStream_t s, int64_t rows, int k, int ldk, uint64_t seed, int table,

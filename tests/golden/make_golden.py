@@ -455,6 +455,71 @@ def g10():
     ref.set_thread_count(1)
 
 
+def g11():
+    """Round 4.  (a) G4 (ML-100K, k = 10) regenerated over thread counts
+    {1, 2, 3, 4, 6, 8} (30 runs: six per seed sample the reference's
+    within-seed chaos, which the per-seed GPU test allows); (b) C2 itself
+    (BASELINE.json configs[1]): the ML-100K generator shrunk at k = 32
+    (users >= 33 ratings, movies >= 32), seed-0 factors, max_iteration 2, 4
+    and the natural stop, with the reference's thread-count spread over
+    {1, 2, 3, 4, 6, 8} recorded (tc_spread) -- the tolerance a GPU run of it
+    can be held to beside 1e-5."""
+    k = 10
+    rs_ = synth.movielens_like("ml-100k", k, seed=synth.DATA_SEED, test_ratio=0.2)
+    runs = []
+    tcs = (1, 2, 3, 4, 6, 8)
+    for seed in range(5):
+        U0, V0 = ref.init_factors(rs_.num_users, rs_.num_items, k, seed)
+        for tc in tcs:
+            ref.set_thread_count(tc)
+            U, V, ret = ref.als(rs_.user_ids, rs_.item_ids, rs_.ratings, k, U0, V0)
+            runs.append(dict(
+                seed=seed, tc=tc, ret=ret,
+                train_rmse=als_oracle.rmse(U, V, rs_.user_ids, rs_.item_ids, rs_.ratings, k),
+                test_rmse=als_oracle.rmse(U, V, rs_.test_user_ids, rs_.test_item_ids,
+                                          rs_.test_ratings, k)))
+    tr = np.array([r["test_rmse"] for r in runs])
+    trn = np.array([r["train_rmse"] for r in runs])
+    band = dict(shape="ml-100k", k=k, data_seed=synth.DATA_SEED, test_ratio=0.2,
+                n_train=int(rs_.n), n_test=int(len(rs_.test_ratings)),
+                num_users=rs_.num_users, num_items=rs_.num_items,
+                ratings_checksum=float(np.sum(rs_.ratings)), thread_counts=list(tcs),
+                runs=runs,
+                test_rmse_min=float(tr.min()), test_rmse_max=float(tr.max()),
+                test_rmse_mean=float(tr.mean()), test_rmse_std=float(tr.std()),
+                train_rmse_min=float(trn.min()), train_rmse_max=float(trn.max()),
+                train_rmse_mean=float(trn.mean()), train_rmse_std=float(trn.std()),
+                meta=_meta(None))
+    with open(os.path.join(HERE, "band_ml100k_k10.json"), "w") as f:
+        json.dump(band, f, indent=1)
+    print("G11 band test rmse", tr.min(), tr.max(), "train", trn.min(), trn.max())
+    k = 32
+    rs_ = synth.movielens_like("ml-100k", k, seed=synth.DATA_SEED)
+    U0, V0 = ref.init_factors(rs_.num_users, rs_.num_items, k, 0)
+    for n_it in (2, 4, 200):
+        res = {}
+        for tc in tcs:
+            ref.set_thread_count(tc)
+            res[tc] = ref.als(rs_.user_ids, rs_.item_ids, rs_.ratings, k, U0, V0,
+                              max_iteration=n_it)
+        U, V, ret = res[1]
+        spread = max(max(np.max(np.abs(res[tc][0] - U)) / np.max(np.abs(U)),
+                         np.max(np.abs(res[tc][1] - V)) / np.max(np.abs(V))) for tc in tcs)
+        rets = {tc: res[tc][2] for tc in tcs}
+        trmse = {tc: als_oracle.rmse(res[tc][0], res[tc][1], rs_.user_ids, rs_.item_ids,
+                                     rs_.ratings, k) for tc in tcs}
+        name = f"als_c2_ml100k_k32_it{n_it}.npz"
+        np.savez_compressed(os.path.join(HERE, name), user_ids=rs_.user_ids,
+                            item_ids=rs_.item_ids, ratings=rs_.ratings, k=k,
+                            num_users=rs_.num_users, num_items=rs_.num_items, U0=U0, V0=V0,
+                            U=U, V=V, ret=ret, tc_spread=spread,
+                            rets_by_tc=json.dumps(rets), train_rmse_by_tc=json.dumps(trmse),
+                            meta=json.dumps(_meta(1)))
+        print("G11", name, "N", rs_.n, rs_.num_users, rs_.num_items, "ret", ret,
+              "rets", rets, "tc spread", spread)
+    ref.set_thread_count(1)
+
+
 if __name__ == "__main__":
     steps = sys.argv[1:] or ["g1", "g2", "g3", "g4", "g5", "g6", "g7", "g8"]
     for s in steps:

@@ -460,9 +460,15 @@ def test_cholesky_mode_vs_oracle(gpu, k):
 
 
 def test_band_realistic_heldout_rmse(gpu):
-    """Ill-conditioned MovieLens-shaped data: the reference itself moves by
-    tens of percent across thread counts, so parity is the reference's own
-    held-out RMSE band (G4: 5 seeds x thread counts 1, 2, 8)."""
+    """C1-shaped ill-conditioned data (ML-100K generator, k = 10, 20 % held
+    out): the reference itself moves by up to 0.13 in held-out RMSE between
+    its own thread counts at one seed, so parity is the reference's band --
+    per seed (round 4): each of the 5 seeds' GPU held-out
+    and train RMSE must lie inside THAT seed's range over the reference's 6
+    thread counts (band_ml100k_k10.json, 30 runs, make_golden.py g11),
+    widened by W, the largest range the reference shows between thread
+    counts at any one seed; the GPU values are reported in a warning."""
+    import warnings
     from movie_recommender_amd import synth
     from movie_recommender_amd.engine import AlsContext
     from oracle import als_oracle as O
@@ -472,18 +478,94 @@ def test_band_realistic_heldout_rmse(gpu):
     k = band["k"]
     rs = synth.movielens_like(band["shape"], k, seed=band["data_seed"],
                               test_ratio=band["test_ratio"])
-    lo = band["test_rmse_min"] - 3 * band["test_rmse_std"]
-    hi = band["test_rmse_max"] + 3 * band["test_rmse_std"]
-    vals = []
-    for seed in range(3):
+    assert rs.n == band["n_train"] and abs(float(np.sum(rs.ratings)) - band["ratings_checksum"]) < 1e-6
+    assert len(band["runs"]) >= 30
+    seeds = sorted({r["seed"] for r in band["runs"]})
+    metrics = ("test_rmse", "train_rmse")
+    chaos = {m: max(max(r[m] for r in band["runs"] if r["seed"] == sd)
+                    - min(r[m] for r in band["runs"] if r["seed"] == sd) for sd in seeds)
+             for m in metrics}
+    report = []
+    for seed in seeds:
         U0, V0 = init_factors(rs.num_users, rs.num_items, k, seed)
         with AlsContext(rs.user_ids, rs.item_ids, rs.ratings, k, rs.num_users,
                         rs.num_items) as ctx:
             ctx.set_factors(U0, V0)
-            ctx.run()
+            ret = ctx.run()
             U, V = ctx.get_factors()
-        vals.append(O.rmse(U, V, rs.test_user_ids, rs.test_item_ids, rs.test_ratings, k))
-    assert lo <= np.mean(vals) <= hi, (vals, lo, hi)
+        vals = {"test_rmse": O.rmse(U, V, rs.test_user_ids, rs.test_item_ids, rs.test_ratings, k),
+                "train_rmse": O.rmse(U, V, rs.user_ids, rs.item_ids, rs.ratings, k)}
+        runs = [r for r in band["runs"] if r["seed"] == seed]
+        report.append(f"seed {seed}: GPU ret {ret} held-out {vals['test_rmse']:.4f} (reference "
+                      f"{min(r['test_rmse'] for r in runs):.4f} .. "
+                      f"{max(r['test_rmse'] for r in runs):.4f}) train {vals['train_rmse']:.4f} "
+                      f"(reference {min(r['train_rmse'] for r in runs):.4f} .. "
+                      f"{max(r['train_rmse'] for r in runs):.4f})")
+        print(report[-1], flush=True)
+        for m in metrics:
+            lo, hi = min(r[m] for r in runs), max(r[m] for r in runs)
+            assert lo - chaos[m] <= vals[m] <= hi + chaos[m], (seed, m, vals[m], lo, hi, chaos[m])
+    warnings.warn("ML-100K band (k=10, %d reference runs; within-seed chaos W: held-out %.4f, "
+                  "train %.4f): " % (len(band["runs"]), chaos["test_rmse"], chaos["train_rmse"])
+                  + "; ".join(report))
+
+
+@pytest.mark.parametrize("name", ["als_c2_ml100k_k32_it2.npz", "als_c2_ml100k_k32_it200.npz"])
+def test_c2_ml100k_k32_through_abi(gpu, name):
+    """C2 itself (BASELINE.json configs[1]: the ML-100K generator shrunk at
+    k = 32, 23,350 ratings, 331 users x 296 movies) through the drop-in
+    als_from_python.  Not pinnable at 1e-5: the compiled reference moves its
+    own factors by 57 % (2 iterations) to 85 % (natural stop) between thread
+    counts 1..8 (tc_spread; 18 % / 60 % after ONE iteration) -- every user
+    block is ill-conditioned and the CG's stagnation stop amplifies summation
+    order.  Pinned instead: `ret` is one the reference returns at some thread
+    count, and the train RMSE lies in the reference's range over its 6 thread
+    counts widened by that range (make_golden.py g11).  The CG arithmetic
+    itself is pinned on this data by test_c2_cg_trace_vs_oracle."""
+    from movie_recommender_amd import _lib
+    d = load_golden(name)
+    from oracle import als_oracle as O
+    k = int(d["k"])
+    assert (len(d["ratings"]), int(d["num_users"]), int(d["num_items"])) == (23350, 331, 296)
+    U, V, ret = abi_als(_lib.lib(), d, max_iteration_of(name, d))
+    rets = set(json.loads(str(d["rets_by_tc"])).values())
+    tr = list(json.loads(str(d["train_rmse_by_tc"])).values())
+    assert ret in rets, (ret, rets)
+    got = O.rmse(U, V, d["user_ids"], d["item_ids"], d["ratings"], k)
+    lo, hi = min(tr), max(tr)
+    assert lo - (hi - lo) <= got <= hi + (hi - lo), (got, lo, hi)
+    print(f"C2 {name}: GPU ret {ret} train RMSE {got:.5f}; reference rets {sorted(rets)} "
+          f"train RMSE {lo:.5f} .. {hi:.5f}")
+
+
+@pytest.mark.parametrize("side", ["users", "items"])
+def test_c2_cg_trace_vs_oracle(gpu, side):
+    """C2's first CG solves (users from U0 / V0, then items from the GPU's
+    solved U) against the oracle's fp64 CG (matrix.cpp:456-529 in block form)
+    on the GPU's own normal equations: the CG count and rr after m = 1, 2, 4,
+    8 iterations and at the natural stop, while the two trajectories can
+    agree (the reference's thread counts themselves part after ~10-20
+    iterations on this data): iterations equal, rr within 1e-10 for m <= 8."""
+    from movie_recommender_amd.engine import AlsContext
+    from oracle import als_oracle as O
+    d = load_golden("als_c2_ml100k_k32_it2.npz")
+    k, nU, nI = int(d["k"]), int(d["num_users"]), int(d["num_items"])
+    with AlsContext(d["user_ids"], d["item_ids"], d["ratings"], k, nU, nI) as ctx:
+        ctx.set_factors(d["U0"], d["V0"])
+        if side == "items":
+            ctx.half_step("users")
+        U1, V1 = ctx.get_factors()
+        nE = nU if side == "users" else nI
+        ctx.build_normal_equations(side)
+        G, c = ctx.normal_equations(side, np.arange(nE))
+        x0 = (U1 if side == "users" else V1).astype(np.float32)
+        for m in (1, 2, 4, 8):
+            ctx.set_factors(U1, V1)
+            its, rr = ctx.half_step(side, 0.01, m)
+            x = x0.copy()     # fp32, as the factor table: x += alpha p rounded
+            ito, rro = O.cg_blocks(G, c, x, 0.01, m)
+            assert its == ito, (side, m, its, ito)
+            assert abs(rr - rro) <= 1e-10 * abs(rro), (side, m, rr, rro)
 
 
 def _gpu_rank_agreement(rs, U, V, k):

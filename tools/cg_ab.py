@@ -5,8 +5,14 @@ ALS iterations; reports per side the solve time per CG iteration (HIP-event
 span of the solve phase / M) and the per-class kernel means.
 
     python tools/cg_ab.py [--k 64] [--m 20] [--reps 3] [--onepass 0|1] [--tag NAME]
-                          [--opt gram_rhs_mfma=0 ...]
-(MR_LIB_PATH selects a variant library, tools/build_var.sh)"""
+                          [--opt gram_rhs_mfma=0 ...] [--shard R/N]
+(MR_LIB_PATH selects a variant library, tools/build_var.sh)
+
+``--shard R/N``: one rank's share of an N-rank run on this one GPU -- a shard
+context over rank R's cost-balanced users and items (distributed.shard_views)
+with no transport attached, so the CG scalars stay local: the per-rank
+kernel work of the sharded run without its exchanges (the collective model's
+"compute per rank")."""
 import argparse
 import json
 import os
@@ -28,6 +34,7 @@ ap.add_argument("--onepass", type=int, default=1)
 ap.add_argument("--tag", default="")
 ap.add_argument("--opt", action="append", default=[],
                 help="engine option NAME=VALUE (engine.OPTIONS), repeatable")
+ap.add_argument("--shard", default=None, help="R/N: rank R's share of an N-rank run")
 a = ap.parse_args()
 rs = load_data("ml-full", a.k)
 rng = np.random.RandomState(0)
@@ -35,7 +42,19 @@ U0 = rng.uniform(-1, 1, rs.num_users * (a.k + 1))
 V0 = rng.uniform(-1, 1, rs.num_items * a.k)
 out = {"tag": a.tag or os.environ.get("MR_LIB_PATH", "default"), "k": a.k, "m": a.m,
        "onepass": a.onepass}
-with AlsContext(rs.user_ids, rs.item_ids, rs.ratings, a.k, rs.num_users, rs.num_items) as ctx:
+if a.shard:
+    from movie_recommender_amd.distributed import shard_views
+    R, N = (int(x) for x in a.shard.split("/"))
+    ur, ir, uv, iv, _, _ = shard_views(rs.user_ids, rs.item_ids, rs.ratings, rs.num_users,
+                                       rs.num_items, R, N, k=a.k)
+    out["shard"] = {"rank": R, "world": N, "users": list(ur), "items": list(ir),
+                    "user_ratings": int(len(uv[0])), "item_ratings": int(len(iv[0]))}
+    make = lambda: AlsContext(uv[0], uv[1], uv[2], a.k, rs.num_users, rs.num_items,  # noqa
+                              user_range=ur, item_range=ir, item_view=iv)
+else:
+    make = lambda: AlsContext(rs.user_ids, rs.item_ids, rs.ratings, a.k, rs.num_users,  # noqa
+                              rs.num_items)
+with make() as ctx:
     ctx.set_option("cg_onepass", a.onepass)
     for o in a.opt:
         name, val = o.split("=")
