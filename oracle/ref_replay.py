@@ -27,11 +27,14 @@ from . import ref
 
 
 def als_replay(user_ids, item_ids, ratings, k, U0, V0, min_r_decrease=0.01,
-               max_iteration=200, on_iteration=None):
+               max_iteration=200, on_iteration=None, on_half_step=None):
     """Returns ``(U, V, ret, trace)``; ``trace`` has one dict per ALS
     iteration: ``cg_users``, ``cg_items`` (iterations), ``t_users``,
     ``t_items`` (seconds inside the reference CG), ``rr``.
-    ``on_iteration(it, record)`` is called after each iteration (progress)."""
+    ``on_iteration(it, record)`` is called after each iteration (progress);
+    ``on_half_step(side, it, U, V)`` before each CG solve with the state it
+    starts from (fp64 tables, not to be modified) -- a caller can run another
+    solver from the reference's own state."""
     uid = np.ascontiguousarray(user_ids, np.int32)
     iid = np.ascontiguousarray(item_ids, np.int32)
     r = np.ascontiguousarray(ratings, np.float64)
@@ -57,12 +60,16 @@ def als_replay(user_ids, item_ids, ratings, k, U0, V0, min_r_decrease=0.01,
     trace = []
     it, old_rr = 0, 0.0
     while it < max_iteration:
+        if on_half_step is not None:
+            on_half_step("users", it, U, V)
         t0 = time.perf_counter()
         x, cu, _ = ref.cg_least_squares(rp_u, ci_u, va_u.reshape(-1), len(U), r, U)
         t_u = time.perf_counter() - t0
         U[:] = x
         va_i[:, :] = Um[uid, :k]                       # fill_item_A (refresh)
         b = r - Um[uid, k]                             # fill_ratings_minus_bias
+        if on_half_step is not None:
+            on_half_step("items", it, U, V)
         t0 = time.perf_counter()
         x, ci, rr = ref.cg_least_squares(rp_i, ci_i, va_i.reshape(-1), len(V), b, V)
         t_i = time.perf_counter() - t0

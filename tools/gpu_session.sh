@@ -13,6 +13,8 @@
 #   stats=ARGS          rocprofv3 --kernel-trace --stats over bench.py ARGS
 #   pmc=CTRS@ARGS       rocprofv3 --pmc CTRS (space-separated) over bench.py ARGS
 #   py=SCRIPT ARGS      python SCRIPT ARGS         -> py_<i>.log
+#   setenv=VAR=VALUE    export VAR for the following steps (e.g. MR_LIB_PATH=...)
+#   unsetenv=VAR        unset it
 # ARGS are split on spaces.  MR_LIB_PATH in the environment selects a variant
 # library (movie_recommender_amd/_lib.py).
 set -o pipefail
@@ -60,6 +62,8 @@ for step in "$@"; do
     py)
       timeout -k 10 900 python -u $arg > $OUT/py_$i.log 2>&1
       rc=$?; tail -5 $OUT/py_$i.log; [ $rc -ne 0 ] && stop py $rc ;;
+    setenv) export "$arg" ;;
+    unsetenv) unset "$arg" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
