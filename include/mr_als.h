@@ -192,10 +192,17 @@ int mr_als_set_timing(mr_als* ctx, int enable);
  *                         chunk's partial sums are order-independent terms)
  *   MR_OPT_PEER_TIMEOUT_S device wait for a peer rank's record in the peer
  *                         all-reduce, seconds (default 30, at most 1e5); on
- *                         expiry the solve ends with an error (< 0) */
+ *                         expiry the solve ends with an error (< 0)
+ *   MR_OPT_CG_TILE_NT     cache policy of the one-pass kernel's normal-
+ *                         equation loads: -1 (default) by size -- non-
+ *                         temporal when a side's per-iteration stream exceeds
+ *                         160 MiB, else the default policy (a shard's side
+ *                         can stay in the Infinity Cache between sweeps);
+ *                         0 always default; 1 always non-temporal.  Results
+ *                         are identical in every mode */
 enum { MR_OPT_FUSE_START = 0, MR_OPT_CG_SPECULATE = 1, MR_OPT_WAIT_TIMEOUT_S = 2,
        MR_OPT_CG_ONEPASS = 3, MR_OPT_GRAM_RHS_MFMA = 4, MR_OPT_CG_SWEEP = 5,
-       MR_OPT_PEER_TIMEOUT_S = 6 };
+       MR_OPT_PEER_TIMEOUT_S = 6, MR_OPT_CG_TILE_NT = 7 };
 int mr_als_set_option(mr_als* ctx, int option, double value);
 /* Ratings per Gram work item: heavier entities are split across waves and
  * their partial normal equations combined in order.  Applies to contexts

@@ -307,6 +307,10 @@ int mr_als_set_option(mr_als* ctx, int option, double value) {
       MR_CHECK(value > 0.0, "timeout must be > 0");
       ctx->eng.wait_timeout_s = value;
       return 0;
+    case MR_OPT_CG_TILE_NT:
+      MR_CHECK(value == -1.0 || value == 0.0 || value == 1.0, "cg_tile_nt must be -1, 0 or 1");
+      ctx->eng.tile_nt = (int)value;
+      return 0;
     case MR_OPT_PEER_TIMEOUT_S:
       return guarded([&]() { return ctx->eng.set_peer_timeout(value); });
     default: MR_CHECK(false, "unknown option");

@@ -85,6 +85,8 @@ struct Engine {
   bool onepass = true;      // one kernel per CG iteration (MR_OPT_CG_ONEPASS)
   bool rhs_mfma = true;     // user-side rhs on the matrix cores (MR_OPT_GRAM_RHS_MFMA)
   int sweep = 1;            // one-pass sweep direction per iteration (MR_OPT_CG_SWEEP)
+  int tile_nt = -1;         // one-pass G tile loads: -1 by size, 0 default policy, 1
+                            // non-temporal (MR_OPT_CG_TILE_NT)
   bool w_bf16 = false;      // every user-view rating is exact in bf16 (set by init)
   int speculate = 1;        // 0: never enqueue ahead; 1: enqueue t+2 while t+1 runs when
                             // state t proves t+1 cannot stop; 2: always one ahead
@@ -133,6 +135,7 @@ struct Engine {
   int peer_handle(unsigned char* out64);
   int set_peer(const unsigned char* handles, int rank, int world);
   int set_peer_timeout(double seconds);
+  bool tile_nt_for(const Side& S) const;
   int weights_bf16(int force);
   int peer_selftest();
   int peer_latency(int iters, double* us);

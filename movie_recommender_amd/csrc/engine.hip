@@ -597,6 +597,20 @@ int Engine::set_peer(const unsigned char* handles, int rank, int world) {
   return 0;
 }
 
+// Cache policy of the one-pass kernel's G tile loads for side S: a side
+// whose per-iteration stream (tri16 blocks + the fp64 CG vectors) exceeds
+// kTileNtBytes is streamed non-temporally -- nothing of it survives in the
+// 256 MiB Infinity Cache to the next sweep anyway, and plain loads measured
+// 25 % slower at the full ML-full users side (DESIGN.md "Sweep direction");
+// a smaller side (a shard of an 8-GPU run) keeps the default policy, so the
+// alternating sweeps can find the previous sweep's tail on-die.
+constexpr int64_t kTileNtBytes = 160ll << 20;
+bool Engine::tile_nt_for(const Side& S) const {
+  if (tile_nt >= 0) return tile_nt != 0;
+  const int64_t vec = (int64_t)S.E * (ldk + (S.user ? 1 : 0)) * (3 * 8 + 4);
+  return (int64_t)S.E * gsize_of(k) * 4 + vec > kTileNtBytes;
+}
+
 // Device wait for a peer's record, seconds (MR_OPT_PEER_TIMEOUT_S); takes
 // effect at once when the peer all-reduce is already mapped.
 int Engine::set_peer_timeout(double seconds) {
@@ -1138,7 +1152,7 @@ int Engine::cg_onepass(Side& S, double min_dec, int max_it, double* final_rr, bo
     const int rev = sweep == 0 ? 0 : ((t & 1) ^ (sweep == 2 ? 1 : 0));
     if (launch_cg_onepass(stream, user, d_state, t > 0 ? 1 : 0, rev, S.E, k, S.G, S.Gs, S.Gn, S.p,
                           S.pb, S.r, S.rb, S.q, S.qb, xf, xb, xbins, S.n_part_op, d_mirror,
-                          seq_of.back()))
+                          seq_of.back(), tile_nt_for(S)))
       return -1;
     return toc(mv_cls, t, ev);
   };

@@ -2249,10 +2249,11 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 4 : 2)) void cg_matvec_kernel(
 #ifndef MR_OP_WAVES
 #define MR_OP_WAVES 4
 #endif
-#ifndef MR_OP_GNT   // non-temporal G tile loads in the one-pass kernel
-#define MR_OP_GNT 1
-#endif
-template <int NB, bool USER>
+// NT: the G tiles are loaded non-temporally (a side whose per-iteration
+// stream is far larger than the Infinity Cache: nothing of it survives to the
+// next sweep) or with the default policy (a shard small enough to stay
+// on-die between sweeps); the engine picks per side (Engine::tile_nt_for)
+template <int NB, bool USER, bool NT>
 __global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 : MR_OP_WAVES) : 2))
 #ifdef MR_OP_WPE
 __attribute__((amdgpu_waves_per_eu(MR_OP_WPE, MR_OP_WPE)))
@@ -2325,7 +2326,7 @@ void cg_onepass_kernel(
       float4 g[NTILE];
 #pragma unroll
       for (int t = 0; t < NTILE; ++t) {
-        const floatx4 v4 = MR_OP_GNT ? __builtin_nontemporal_load(Ge + t * 64 + lane) : Ge[t * 64 + lane];
+        const floatx4 v4 = NT ? __builtin_nontemporal_load(Ge + t * 64 + lane) : Ge[t * 64 + lane];
         g[t] = make_float4(v4[0], v4[1], v4[2], v4[3]);
       }
       float d2 = 0.f;
@@ -2443,7 +2444,8 @@ int onepass_blocks_per_cu(bool user_side, int k) {
   const void* f = nullptr;
 #define MR_OP_FN(NB)                                                                        \
   case NB:                                                                                  \
-    f = user_side ? (const void*)cg_onepass_kernel<NB, true> : (const void*)cg_onepass_kernel<NB, false>; \
+    f = user_side ? (const void*)cg_onepass_kernel<NB, true, true>                          \
+                  : (const void*)cg_onepass_kernel<NB, false, true>;                        \
     break;
   switch (nb16_of(k)) {
     MR_OP_FN(1) MR_OP_FN(2) MR_OP_FN(3) MR_OP_FN(4)
@@ -2459,17 +2461,18 @@ int onepass_blocks_per_cu(bool user_side, int k) {
 int launch_cg_onepass(hipStream_t s, bool user_side, CgState* st, int update, int rev, int64_t E, int k,
                       const float* G, const float* Gs, const float* Gn, double* p, double* pb,
                       double* r, double* rb, double* q, double* qb, float* x, float* xb,
-                      int64_t* xbins, int n_part, CgMirror* mirror, int seq) {
+                      int64_t* xbins, int n_part, CgMirror* mirror, int seq, bool nt) {
   if (n_part <= 0) return 0;
+#define MR_OP_LAUNCH(NB, U, T)                                                              \
+  MR_LAUNCH((cg_onepass_kernel<NB, U, T>), dim3(n_part), dim3(256), 0, s, st, update, rev, E, k, \
+            ldk_of(k), G, Gs, Gn, p, pb, r, rb, q, qb, x, xb, xbins, mirror, seq)
 #define MR_OP_CASE(NB)                                                                      \
   case NB:                                                                                  \
-    if (user_side)                                                                          \
-      MR_LAUNCH((cg_onepass_kernel<NB, true>), dim3(n_part), dim3(256), 0, s, st, update, rev, \
-                E, k, ldk_of(k), G, Gs, Gn, p, pb, r, rb, q, qb, x, xb, xbins, mirror, seq); \
-    else                                                                                    \
-      MR_LAUNCH((cg_onepass_kernel<NB, false>), dim3(n_part), dim3(256), 0, s, st, update,  \
-                rev, E, k, ldk_of(k), G, Gs, Gn, p, pb, r, rb, q, qb, x, xb, xbins, mirror, \
-                seq);                                                                       \
+    if (user_side) {                                                                        \
+      if (nt) MR_OP_LAUNCH(NB, true, true); else MR_OP_LAUNCH(NB, true, false);             \
+    } else {                                                                                \
+      if (nt) MR_OP_LAUNCH(NB, false, true); else MR_OP_LAUNCH(NB, false, false);           \
+    }                                                                                       \
     break;
   switch (nb16_of(k)) {
     MR_OP_CASE(1) MR_OP_CASE(2) MR_OP_CASE(3) MR_OP_CASE(4)
@@ -2477,6 +2480,7 @@ int launch_cg_onepass(hipStream_t s, bool user_side, CgState* st, int update, in
     default: set_error("one-pass CG needs k <= 128"); return -1;
   }
 #undef MR_OP_CASE
+#undef MR_OP_LAUNCH
   MR_HIP(hipGetLastError());
   return 0;
 }

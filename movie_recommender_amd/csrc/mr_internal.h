@@ -303,8 +303,9 @@ int onepass_blocks_per_cu(bool user_side, int k);
 int launch_cg_onepass(hipStream_t s, bool user_side, CgState* st, int update, int rev, int64_t E, int k,
                       const float* G, const float* Gs, const float* Gn, double* p, double* pb,
                       double* r, double* rb, double* q, double* qb, float* x, float* xb,
-                      int64_t* xbins, int n_part, CgMirror* mirror, int seq);
+                      int64_t* xbins, int n_part, CgMirror* mirror, int seq, bool nt);
 // x is the fp32 factor table (and bias), r / p / q the fp64 CG vectors;
+// nt: non-temporal G tile loads (Engine::tile_nt_for);
 // xbins: kXBins x 4 x 11 int64 bins of the order-independent sums (zero
 // between launches: the last block reads and resets them).
 constexpr int kXBinWords = 16 * 4 * 11;       // kXBins x sums x (kXD + 1), kernels.hip

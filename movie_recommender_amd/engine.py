@@ -14,7 +14,7 @@ from . import _lib
 SOLVERS = {"cg": 0, "cholesky": 1}
 OPTIONS = {"fuse_start": 0, "cg_speculate": 1, "wait_timeout_s": 2,
            "cg_onepass": 3, "gram_rhs_mfma": 4, "cg_sweep": 5,
-           "peer_timeout_s": 6}   # include/mr_als.h
+           "peer_timeout_s": 6, "cg_tile_nt": 7}   # include/mr_als.h
 
 
 def _i32(a):

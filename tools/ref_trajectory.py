@@ -33,19 +33,20 @@ def main():
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--k", type=int, default=64)
     ap.add_argument("--shape", default="ml-full")
+    ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r04",
                                                   "ref_trajectory_c3_k64.jsonl"))
     a = ap.parse_args()
     import bench
     rs = bench.load_data(a.shape, a.k)
-    U0, V0 = ref.init_factors(rs.num_users, rs.num_items, a.k, 0)
+    U0, V0 = ref.init_factors(rs.num_users, rs.num_items, a.k, a.seed)
     ref.set_thread_count(a.threads)
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     t0 = time.time()
     with open(a.out, "w") as f:
         f.write(json.dumps({"shape": a.shape, "k": a.k, "n": rs.n, "users": rs.num_users,
                             "items": rs.num_items, "threads": a.threads,
-                            "start": "RandomState(0) U0, V0 (bench.py)",
+                            "start": f"RandomState({a.seed}) U0, V0 (bench.py: 0)",
                             "outer_stop": "off (min_r_decrease=-inf)"}) + "\n")
         f.flush()
 
