@@ -26,15 +26,27 @@ import numpy as np
 from . import ref
 
 
+def _alt(threads, rp, ci, va, ncols, b, x0):
+    keep = ref.lib().get_thread_count()
+    ref.set_thread_count(threads)
+    try:
+        _, its, rr = ref.cg_least_squares(rp, ci, va.reshape(-1), ncols, b, x0)
+    finally:
+        ref.set_thread_count(keep)
+    return its, rr
+
+
 def als_replay(user_ids, item_ids, ratings, k, U0, V0, min_r_decrease=0.01,
                max_iteration=200, on_iteration=None, on_half_step=None):
     """Returns ``(U, V, ret, trace)``; ``trace`` has one dict per ALS
     iteration: ``cg_users``, ``cg_items`` (iterations), ``t_users``,
     ``t_items`` (seconds inside the reference CG), ``rr``.
     ``on_iteration(it, record)`` is called after each iteration (progress);
-    ``on_half_step(side, it, U, V)`` before each CG solve with the state it
-    starts from (fp64 tables, not to be modified) -- a caller can run another
-    solver from the reference's own state."""
+    ``on_half_step(side, it, U, V, alt)`` before each CG solve with the state
+    it starts from (fp64 tables, not to be modified) -- a caller can run
+    another solver from the reference's own state; ``alt(threads)`` runs the
+    reference's same solve at another thread count and returns
+    ``(iterations, final_rr)`` (the reference's own summation-order spread)."""
     uid = np.ascontiguousarray(user_ids, np.int32)
     iid = np.ascontiguousarray(item_ids, np.int32)
     r = np.ascontiguousarray(ratings, np.float64)
@@ -61,7 +73,8 @@ def als_replay(user_ids, item_ids, ratings, k, U0, V0, min_r_decrease=0.01,
     it, old_rr = 0, 0.0
     while it < max_iteration:
         if on_half_step is not None:
-            on_half_step("users", it, U, V)
+            on_half_step("users", it, U, V, lambda tc: _alt(
+                tc, rp_u, ci_u, va_u, len(U), r, U))
         t0 = time.perf_counter()
         x, cu, _ = ref.cg_least_squares(rp_u, ci_u, va_u.reshape(-1), len(U), r, U)
         t_u = time.perf_counter() - t0
@@ -69,7 +82,8 @@ def als_replay(user_ids, item_ids, ratings, k, U0, V0, min_r_decrease=0.01,
         va_i[:, :] = Um[uid, :k]                       # fill_item_A (refresh)
         b = r - Um[uid, k]                             # fill_ratings_minus_bias
         if on_half_step is not None:
-            on_half_step("items", it, U, V)
+            on_half_step("items", it, U, V, lambda tc: _alt(
+                tc, rp_i, ci_i, va_i, len(V), b, V))
         t0 = time.perf_counter()
         x, ci, rr = ref.cg_least_squares(rp_i, ci_i, va_i.reshape(-1), len(V), b, V)
         t_i = time.perf_counter() - t0

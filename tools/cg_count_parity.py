@@ -15,7 +15,10 @@ CG defaults (0.01, 200); its CG iteration count and final rr are recorded
 beside the reference's.  Two runs of a chaotic trajectory part after a few
 iterations (the reference's own thread counts do), so counts over a window
 of two trajectories compare draws; from the same state they compare the
-solvers.  One JSON line per half-step and a summary line.
+solvers.  With ``--alt-threads T`` every reference solve is also run at T
+threads from the same state: the reference's own summation-order spread of
+the counts, the yardstick for the engine's.  One JSON line per half-step
+and a summary line.
 """
 import argparse
 import json
@@ -29,11 +32,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def run(scale=1.0, iterations=25, threads=None, k=64, seed=0, out=None, log=print):
+def run(scale=1.0, iterations=25, threads=None, k=64, seed=0, out=None, log=print,
+        alt_threads=None, engine=True):
     import bench
     from oracle import ref
     from oracle.ref_replay import als_replay
-    from movie_recommender_amd.engine import AlsContext
+    if engine:
+        from movie_recommender_amd.engine import AlsContext
     rs = bench.load_data("ml-full", k, scale=scale)
     U0, V0 = ref.init_factors(rs.num_users, rs.num_items, k, seed)
     if threads is None:
@@ -41,12 +46,19 @@ def run(scale=1.0, iterations=25, threads=None, k=64, seed=0, out=None, log=prin
     ref.set_thread_count(threads)
     recs = []
     t0 = time.time()
-    with AlsContext(rs.user_ids, rs.item_ids, rs.ratings, k, rs.num_users,
-                    rs.num_items) as ctx:
-        def on_half_step(side, it, U, V):
-            ctx.set_factors(U, V)
-            its, rr = ctx.half_step(side)
-            recs.append({"iteration": it + 1, "side": side, "engine": [its, rr]})
+    import contextlib
+    with (AlsContext(rs.user_ids, rs.item_ids, rs.ratings, k, rs.num_users, rs.num_items)
+          if engine else contextlib.nullcontext()) as ctx:
+        def on_half_step(side, it, U, V, alt):
+            if engine:
+                ctx.set_factors(U, V)
+                its, rr = ctx.half_step(side)
+            else:   # CPU exploration: the reference's own spread only
+                its, rr = -1, float("nan")
+            rec = {"iteration": it + 1, "side": side, "engine": [its, rr]}
+            if alt_threads:
+                rec["reference_alt"] = list(alt(alt_threads))
+            recs.append(rec)
 
         def on_iteration(it, rec):
             for r in recs[-2:]:
@@ -64,13 +76,21 @@ def run(scale=1.0, iterations=25, threads=None, k=64, seed=0, out=None, log=prin
                    on_half_step=on_half_step)
     ref.set_thread_count(1)
     summ = {"scale": scale, "k": k, "n": int(rs.n), "iterations": iterations,
-            "threads": threads}
+            "threads": threads, "alt_threads": alt_threads}
     for side in ("users", "items"):
         rr = [r for r in recs if r["side"] == side]
         eq = sum(r["engine"][0] == r["reference"][0] for r in rr)
         summ[side] = {"half_steps": len(rr), "equal_counts": eq,
                       "engine_total": sum(r["engine"][0] for r in rr),
-                      "reference_total": sum(r["reference"][0] for r in rr)}
+                      "reference_total": sum(r["reference"][0] for r in rr),
+                      "unequal": [[r["iteration"], r["engine"][0], r["reference"][0]]
+                                  for r in rr if r["engine"][0] != r["reference"][0]]}
+        if alt_threads:
+            summ[side]["reference_alt_equal_counts"] = sum(
+                r["reference_alt"][0] == r["reference"][0] for r in rr)
+            summ[side]["reference_alt_unequal"] = [
+                [r["iteration"], r["reference_alt"][0], r["reference"][0]]
+                for r in rr if r["reference_alt"][0] != r["reference"][0]]
         if side == "items":
             rel = [abs(r["engine"][1] - r["reference"][1]) / abs(r["reference"][1]) for r in rr
                    if r["engine"][0] == r["reference"][0]]
@@ -83,11 +103,15 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--iterations", type=int, default=25)
     ap.add_argument("--threads", type=int, default=None)
+    ap.add_argument("--alt-threads", type=int, default=None,
+                    help="also run each reference solve at this thread count (its own spread)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--no-engine", action="store_true", help="reference spread only (CPU)")
     a = ap.parse_args()
     f = open(a.out, "w") if a.out else None
     _, summ = run(a.scale, a.iterations, a.threads, out=f,
-                  log=lambda m: print(m, file=sys.stderr, flush=True))
+                  log=lambda m: print(m, file=sys.stderr, flush=True), alt_threads=a.alt_threads,
+                  engine=not a.no_engine)
     line = json.dumps({"summary": summ})
     print(line, flush=True)
     if f:

@@ -44,13 +44,14 @@ def main():
     ap.add_argument("--threads", type=int, default=6)
     ap.add_argument("--k", type=int, default=64)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r04",
                                                   "cg_precision_probe.jsonl"))
     a = ap.parse_args()
     import bench
     k = a.k
     K = k + 1
-    rs = bench.load_data("ml-full", k)
+    rs = bench.load_data("ml-full", k, scale=a.scale)
     U0, V0 = ref.init_factors(rs.num_users, rs.num_items, k, a.seed)
     ref.set_thread_count(a.threads)
     uid = np.ascontiguousarray(rs.user_ids, np.int32)
