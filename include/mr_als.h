@@ -196,7 +196,7 @@ int mr_als_set_timing(mr_als* ctx, int enable);
  *   MR_OPT_CG_TILE_NT     cache policy of the one-pass kernel's normal-
  *                         equation loads: -1 (default) by size -- non-
  *                         temporal when a side's per-iteration stream exceeds
- *                         160 MiB, else the default policy (a shard's side
+ *                         320 MiB, else the default policy (a shard's side
  *                         can stay in the Infinity Cache between sweeps);
  *                         0 always default; 1 always non-temporal.  Results
  *                         are identical in every mode */

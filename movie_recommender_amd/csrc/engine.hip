@@ -599,12 +599,14 @@ int Engine::set_peer(const unsigned char* handles, int rank, int world) {
 
 // Cache policy of the one-pass kernel's G tile loads for side S: a side
 // whose per-iteration stream (tri16 blocks + the fp64 CG vectors) exceeds
-// kTileNtBytes is streamed non-temporally -- nothing of it survives in the
-// 256 MiB Infinity Cache to the next sweep anyway, and plain loads measured
-// 25 % slower at the full ML-full users side (DESIGN.md "Sweep direction");
-// a smaller side (a shard of an 8-GPU run) keeps the default policy, so the
-// alternating sweeps can find the previous sweep's tail on-die.
-constexpr int64_t kTileNtBytes = 160ll << 20;
+// kTileNtBytes is streamed non-temporally -- little of it survives in the
+// 256 MiB Infinity Cache to the next sweep, and plain loads measured 25 %
+// slower at the full ML-full users side (1.26 GB; DESIGN.md "Sweep
+// direction"); a smaller side keeps the default policy, so the alternating
+// sweeps find the previous sweep's tail on-die: measured 5-6 % faster at the
+// 4- and 8-rank shard sizes of ML-full (users 260 / 157 MB per iteration,
+// profiles/r04 session r04b).
+constexpr int64_t kTileNtBytes = 320ll << 20;
 bool Engine::tile_nt_for(const Side& S) const {
   if (tile_nt >= 0) return tile_nt != 0;
   const int64_t vec = (int64_t)S.E * (ldk + (S.user ? 1 : 0)) * (3 * 8 + 4);

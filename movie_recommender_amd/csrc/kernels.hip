@@ -2253,8 +2253,14 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 4 : 2)) void cg_matvec_kernel(
 // stream is far larger than the Infinity Cache: nothing of it survives to the
 // next sweep) or with the default policy (a shard small enough to stay
 // on-die between sweeps); the engine picks per side (Engine::tile_nt_for)
-template <int NB, bool USER, bool NT>
-__global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 : MR_OP_WAVES) : 2))
+#ifndef MR_OP_LOOKAHEAD   // entity e + 1's operands loaded while e is processed (NB <= 4)
+#define MR_OP_LOOKAHEAD 0
+#endif
+#ifndef MR_OP_LA_WAVES    // waves per SIMD the lookahead form is bounded to
+#define MR_OP_LA_WAVES 3
+#endif
+template <int NB, bool USER, bool NT, bool LA = (MR_OP_LOOKAHEAD != 0 && NB <= 4)>
+__global__ __launch_bounds__(256, (NB <= 4 ? (LA ? MR_OP_LA_WAVES : (USER && NB == 4 ? MR_OP_WAVES_U4 : MR_OP_WAVES)) : 2))
 #ifdef MR_OP_WPE
 __attribute__((amdgpu_waves_per_eu(MR_OP_WPE, MR_OP_WPE)))
 #endif
@@ -2297,50 +2303,66 @@ void cg_onepass_kernel(
     const int64_t c1 = c0 + XC < E ? c0 + XC : E;
     double a = 0.0, b = 0.0, c = 0.0;
     double d = 0.0;   // r.r of the updated residual (matrix.cpp:507's direct dot)
-    for (int64_t e = c0; e < c1; ++e) {
+    // One entity's operands: the CG vectors' entries of this lane, the bias
+    // entries (user side) and the G tiles.  MR_OP_LOOKAHEAD: entity e + 1's
+    // are loaded while entity e is updated and multiplied (one more register
+    // set), so a wave that owns few entities -- a shard of an N-GPU run --
+    // does not pay a full memory latency per entity; same values, same order.
+    struct Ent {
+      double pi[NV], ri[NV], qi[NV];
+      float xi[NV];
+      double pbias, rbias, qbias;
+      float xbias, d2;
+      float4 g[NTILE];
+    };
+    auto load_ent = [&](int64_t e, Ent& E_) {
+      const double* pe = p + e * ldk;
+      const double* re = r + e * ldk;
+      const double* qe = q + e * ldk;
+      const float* xe = x + e * ldk;
+#pragma unroll
+      for (int h = 0; h < NV; ++h) {
+        const int i = lane + 64 * h;
+        E_.pi[h] = (i < NP) ? pe[i] : 0.0;
+        E_.ri[h] = (i < NP) ? re[i] : 0.0;
+        E_.qi[h] = (update && i < NP) ? qe[i] : 0.0;
+        E_.xi[h] = (update && i < NP) ? xe[i] : 0.f;
+      }
+      E_.pbias = E_.rbias = E_.qbias = 0.0;
+      E_.xbias = 0.f;
+      if (USER) {
+        E_.pbias = pb[e];
+        E_.rbias = rb[e];
+        if (update) {
+          E_.qbias = qb[e];
+          E_.xbias = xb[e];
+        }
+      }
+      const floatx4* __restrict__ Ge = reinterpret_cast<const floatx4*>(G + e * GS);
+#pragma unroll
+      for (int t = 0; t < NTILE; ++t) {
+        const floatx4 v4 = NT ? __builtin_nontemporal_load(Ge + t * 64 + lane) : Ge[t * 64 + lane];
+        E_.g[t] = make_float4(v4[0], v4[1], v4[2], v4[3]);
+      }
+      E_.d2 = 0.f;
+      if (NF > 0 && lane < 16 * NF) E_.d2 = G[e * GS + NTILE * 256 + lane];
+    };
+    auto process = [&](int64_t e, const Ent& E_) {
       double* pe = p + e * ldk;
       double* re = r + e * ldk;
       double* qe = q + e * ldk;
       float* xe = x + e * ldk;
-      double pi[NV], ri[NV], qi[NV];
-      float xi[NV];
-#pragma unroll
-      for (int h = 0; h < NV; ++h) {
-        const int i = lane + 64 * h;
-        pi[h] = (i < NP) ? pe[i] : 0.0;
-        ri[h] = (i < NP) ? re[i] : 0.0;
-        qi[h] = (update && i < NP) ? qe[i] : 0.0;
-        xi[h] = (update && i < NP) ? xe[i] : 0.f;
-      }
-      double pbias = 0.0, rbias = 0.0, qbias = 0.0;
-      float xbias = 0.f;
-      if (USER) {
-        pbias = pb[e];
-        rbias = rb[e];
-        if (update) {
-          qbias = qb[e];
-          xbias = xb[e];
-        }
-      }
-      const floatx4* __restrict__ Ge = reinterpret_cast<const floatx4*>(G + e * GS);
-      float4 g[NTILE];
-#pragma unroll
-      for (int t = 0; t < NTILE; ++t) {
-        const floatx4 v4 = NT ? __builtin_nontemporal_load(Ge + t * 64 + lane) : Ge[t * 64 + lane];
-        g[t] = make_float4(v4[0], v4[1], v4[2], v4[3]);
-      }
-      float d2 = 0.f;
-      if (NF > 0 && lane < 16 * NF) d2 = G[e * GS + NTILE * 256 + lane];
+      double pbias = E_.pbias, rbias = E_.rbias;
 #pragma unroll
       for (int h = 0; h < NV; ++h) {
         const int i = lane + 64 * h;
         if (i < NP) {
-          double rn = ri[h], pn = pi[h];
+          double rn = E_.ri[h], pn = E_.pi[h];
           if (update) {
-            rn = fma(alpha, qi[h], ri[h]);
+            rn = fma(alpha, E_.qi[h], E_.ri[h]);
             re[i] = rn;
-            xe[i] = (float)fma(alpha, pi[h], (double)xi[h]);
-            pn = fma(beta, pi[h], -rn);
+            xe[i] = (float)fma(alpha, E_.pi[h], (double)E_.xi[h]);
+            pn = fma(beta, E_.pi[h], -rn);
             pe[i] = pn;
             d = fma(rn, rn, d);
           }
@@ -2349,21 +2371,21 @@ void cg_onepass_kernel(
         }
       }
       if (USER && update) {
-        const double rbn = fma(alpha, qbias, rbias);
+        const double rbn = fma(alpha, E_.qbias, rbias);
         const double pbn = fma(beta, pbias, -rbn);
         if (lane == 0) {
           rb[e] = rbn;
-          xb[e] = (float)fma(alpha, pbias, (double)xbias);
+          xb[e] = (float)fma(alpha, pbias, (double)E_.xbias);
           pb[e] = pbn;
         }
         rbias = rbn;
         pbias = pbn;
         if (lane == 0) d = fma(rbn, rbn, d);
       }
-      if (NF > 0 && lane < 16 * NF) sc.dd[lane] = d2;
+      if (NF > 0 && lane < 16 * NF) sc.dd[lane] = E_.d2;
       __builtin_amdgcn_wave_barrier();
       double yo[NV], ybv = 0.0;
-      tile_matvec<NB, USER, (NB > 4) || MR_OP_OPAQUE>(g, sc, pbias, USER ? Gs + e * ldk : nullptr,
+      tile_matvec<NB, USER, (NB > 4) || MR_OP_OPAQUE>(E_.g, sc, pbias, USER ? Gs + e * ldk : nullptr,
                                                       USER ? Gn[e] : 0.f, k, yo, ybv);
 #pragma unroll
       for (int h = 0; h < NV; ++h) {
@@ -2385,6 +2407,21 @@ void cg_onepass_kernel(
         c = fma(ybv, ybv, c);
       }
       __builtin_amdgcn_wave_barrier();
+    };
+    if constexpr (LA) {
+      Ent cur, nxt;
+      load_ent(c0, cur);
+      for (int64_t e = c0; e < c1; ++e) {
+        if (e + 1 < c1) load_ent(e + 1, nxt);
+        process(e, cur);
+        cur = nxt;
+      }
+    } else {
+      for (int64_t e = c0; e < c1; ++e) {
+        Ent cur;
+        load_ent(e, cur);
+        process(e, cur);
+      }
     }
     a = wave_sum_f64(a);
     b = wave_sum_f64(b);
@@ -3264,6 +3301,9 @@ constexpr int SP_THREADS = 256;
 #define MR_SP_AUX 0
 #endif
 constexpr int SP_TILE = kSpTile;     // staged products per row block (16 KiB fp64)
+#ifndef MR_SP_GPRE   // gathers of the next short block issued before this block's row sums
+#define MR_SP_GPRE 0
+#endif
 
 template <int GATHER, int OUT, bool BUF>
 __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
@@ -3387,9 +3427,15 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
     }
     if (n1 - n0 <= SP_TILE) load_short(cur, r0, r1, n0, n1);
   }
+  // MR_SP_GPRE: the next short block's gathers (its ids arrived with
+  // load_short) are issued behind this block's product stores, so they are
+  // in flight during the barrier and the row sums (same values, same order)
+  double gpre[MR_SP_GPRE ? PER : 1];
+  bool have_pre = false;
   for (; b < n_blk; b += gs) {
     const bool has_next = b + gs < n_blk, has_next2 = b + 2 * gs < n_blk;
-    if (has_next && qn1 - qn0 <= SP_TILE) load_short(nxt, qr0, qr1, qn0, qn1);
+    const bool next_short = has_next && qn1 - qn0 <= SP_TILE;
+    if (next_short) load_short(nxt, qr0, qr1, qn0, qn1);
     int64_t sr0 = 0, sr1 = 0;   // bounds of block b + 2 gs
     if (has_next2) {
       sr0 = blk[b + 2 * gs];
@@ -3397,13 +3443,25 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
     }
     if (n1 - n0 <= SP_TILE) {
       double gx[PER];
+      if (MR_SP_GPRE && have_pre) {
 #pragma unroll
-      for (int u = 0; u < PER; ++u) gx[u] = gather(cur.cc[u]);
+        for (int u = 0; u < PER; ++u) gx[u] = gpre[u];
+      } else {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) gx[u] = gather(cur.cc[u]);
+      }
       const int nl = (int)(n1 - n0);
 #pragma unroll
       for (int u = 0; u < PER; ++u) {
         const int jl = BUF ? 8 * t + u : t + u * SP_THREADS;   // load_short's entry map
         if (jl < nl) prod[jl] = cur.vv[u] * gx[u];
+      }
+      if (MR_SP_GPRE) {
+        have_pre = next_short;
+        if (next_short) {
+#pragma unroll
+          for (int u = 0; u < PER; ++u) gpre[u] = gather(nxt.cc[u]);
+        }
       }
       const int R = (int)(r1 - r0);
       if (t < R) srp[t] = cur.rpo;
@@ -3432,6 +3490,7 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
       if (lr < R && g == 0) emit(r0 + lr, sum);
       __syncthreads();   // prod / srp are reused by the next block
     } else {             // one long row: per-thread strided sums, fixed-order tree
+      if (MR_SP_GPRE) have_pre = false;
       double sum = 0.0;
       for (int64_t j = n0 + t; j < n1; j += SP_THREADS) sum += v[j] * gather(ci[j]);
       sum = block_sum_f64<SP_THREADS>(sum, sh);
