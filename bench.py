@@ -308,7 +308,7 @@ def main():
     ap.add_argument("--device-map", default=None,
                     help="test only: comma-separated GPU index per local rank "
                          "(e.g. 0,0 puts two ranks on GPU 0; needs --comm gloo)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r03.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r04.json"),
                     help="per-kernel HBM bytes from a rocprofv3 --pmc run (optional)")
     args = ap.parse_args()
 
