@@ -1,8 +1,15 @@
 """Headline benchmark: ratings processed per second per ALS iteration
 (BASELINE.json metric), MovieLens-full shape, k = 64, on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--k 64]
+    python bench.py [--gpus N] [--steps 20] [--warmup 5] [--k 64]
                     [--shape ml-full|c5] [--scale S] [--solver cg|cholesky] [--no-cpu]
+                    [--comm rccl|gloo] [--device-map 0,0]
+
+``--gpus N`` (N > 1) without a launcher starts the N ranks itself:
+``torch.distributed.run --nproc-per-node N bench.py ...`` as a child
+process; its ranks' one JSON line is relayed.  Under a launcher,
+``WORLD_SIZE`` must equal ``--gpus``.  ``--comm gloo --device-map 0,0`` (tests
+on a one-GPU box) puts two ranks on GPU 0 with host-staged exchanges.
 
 ``--shape c5`` is BASELINE.json configs[4] (synthetic 10 M users x 1 M items x
 1e9 ratings; use --k 128): streamed by ``synth.C5Generator`` -- every rank
@@ -20,9 +27,13 @@ data set: per-rank work shrinks as N grows -> "strong").
 Printed on rank 0: ONE JSON line with the contract fields plus
 ``roofline`` (dominant kernel, from HIP events on the engine's stream over an
 instrumented replay of the timed steps; the timed region itself carries no
-per-launch events) and ``cpu_baseline`` (the reference library compiled from
-/root/reference sources, oracle/_ref/cpp_ls_lib.so, timed on a bounded
-sample of the same workload; N = 1 only).
+per-launch events), ``cpu_baseline`` (the reference library compiled from
+/root/reference sources, oracle/_ref/cpp_ls_lib.so, timed on the same data
+and start -- full C3 by default, ``--cpu-scale`` shrinks it; N = 1 only),
+``same_window`` (the GPU's iterations 2-3 of the same start, the window the
+CPU leg's T(3) - T(1) times, with both sides' CG counts) and ``trajectory``
+(the CG iterations of every ALS iteration from the start, checked against
+the timed region's totals).
 """
 import argparse
 import json
