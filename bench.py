@@ -549,11 +549,11 @@ def main():
     avg_s = tot_ms / launches / 1e3
     _, nU, _ = ctx.local_size("users")
     _, nI, n_local_items = ctx.local_size("items")
-    # one-pass CG: unsharded or with peer scalars (RCCL collectives: two
-    # kernels), and not on the user side at k > 64 (Engine::cg)
+    # one-pass CG on both sides at k <= 128: unsharded or with peer scalars
+    # (RCCL collectives: two kernels; Engine::onepass_for)
     onepass = (not args.no_onepass and k <= 128
                and (dist is None or getattr(ctx, "peer_scalars", False)))
-    onepass_of = lambda c: onepass and (c.endswith("items") or k <= 64)  # noqa: E731
+    onepass_of = lambda c: onepass  # noqa: E731
     nbytes, nflops = algorithmic_cost(cls, k, nU, nI, n_local_users, ldk, not args.no_fuse_start,
                                       n_local_items, onepass_of(cls))
     bound = "mfma" if cls.startswith("gram") and k >= 32 else "hbm"
@@ -612,8 +612,7 @@ def main():
                                    else "single"),
                    "cg_scalars": ("peer all-reduce (IPC)" if getattr(ctx, "peer_scalars", False)
                                   else "rccl all-reduce" if dist is not None else "local"),
-                   "cg_iteration": ("matvec + update" if not onepass else "one pass"
-                                    if k <= 64 else "one pass (items), matvec + update (users)")},
+                   "cg_iteration": "one pass" if onepass else "matvec + update"},
         "roofline": {"kernel": cls, "bound": bound, "achieved": round(achieved, 2),
                      "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
                      "traffic": traffic,

@@ -175,8 +175,7 @@ int mr_als_set_timing(mr_als* ctx, int enable);
  *   MR_OPT_CG_ONEPASS     1 (default): one kernel per CG iteration (the
  *                         previous iteration's x / r update deferred into
  *                         the next matvec, r'.r' from r.r, r.q, q.q; k <= 128,
- *                         unsharded or peer scalars, not the user side at
- *                         k > 64); 0: matvec + update
+ *                         unsharded or peer scalars); 0: matvec + update
  *   MR_OPT_GRAM_RHS_MFMA  1 (default): the user-side Gram at 64 < k <= 128
  *                         takes its rhs and row sums on the matrix cores when
  *                         every user-view rating is exact in bf16 (half-star

@@ -866,12 +866,12 @@ CgStart Engine::cg_start_of(Side& S) {
 }
 
 bool Engine::onepass_for(const Side& S) const {
-  // one pass per CG iteration everywhere except the user side at k > 64:
-  // there the one-pass kernel (32 tiles + the deferred-update vectors at 2
-  // waves / SIMD) spills 18 registers and measured 3 % slower per CG
-  // iteration than matvec + update (k = 128, ML-full, fixed 20 iterations:
-  // 0.286 vs 0.278 ms); the item side gains 8 % there
-  return onepass && k <= kMaxK && (!S.user || nb16_of(k) <= 4) && (!sharded() || peer_on);
+  // one pass per CG iteration on both sides for k <= 128.  At k > 64 the
+  // tiles stream through a register ring (tile_matvec_stream, no spills):
+  // k = 128, ML-full shape, fixed 20 iterations, users 0.2411 ms per CG
+  // iteration against 0.2617 for matvec + update (0.2724 in round 3's
+  // two-kernel form), items 0.1093 against 0.1356 (profiles/r04 session r04d)
+  return onepass && k <= kMaxK && (!sharded() || peer_on);
 }
 
 // start: the Gram waves also start the CG solve (r0, p0, q0 = G p0 and the

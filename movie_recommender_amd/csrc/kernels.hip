@@ -14,6 +14,7 @@
 //   solve_kernel     exact per-entity Cholesky (north-star "exact" mode)
 // Wave = 64 lanes throughout; no CUDA idioms.
 #include <cstdlib>
+#include <type_traits>
 #include <utility>
 
 #include "mr_internal.h"
@@ -284,13 +285,17 @@ struct MvScratch {
 // row sums and count.  The user-side bias column Gs vb is added to every y.
 // A diagonal block contributes only its stored triangle (the bf16x3 MFMA sum
 // is not bitwise symmetric; mr_internal.h).
+template <int NB, bool USER>
+__device__ __forceinline__ void tile_matvec_finish(MvScratch<NB>& sc, double vb,
+                                                   const float* __restrict__ Gs_e, float gn, int k,
+                                                   double (&yo)[(16 * NB + 63) / 64], double& yb);
+
 template <int NB, bool USER, bool OPAQUE = (NB > 4)>
 __device__ __forceinline__ void tile_matvec(
     const float4 (&g)[NB * (NB - 1) / 2 + NB / 2 + (NB & 1)], MvScratch<NB>& sc, double vb,
     const float* __restrict__ Gs_e, float gn, int k, double (&yo)[(16 * NB + 63) / 64],
     double& yb) {
   constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2;
-  constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
   const int lane = threadIdx.x & 63;
   const int rr = lane >> 2, c4 = (lane & 3) * 4;
   auto tile = [&](int t, double (&ge)[4]) {
@@ -368,6 +373,19 @@ __device__ __forceinline__ void tile_matvec(
     dst[0] = make_double2(cc[0], cc[1]);
     dst[1] = make_double2(cc[2], cc[3]);
   }
+  tile_matvec_finish<NB, USER>(sc, vb, Gs_e, gn, k, yo, yb);
+}
+
+// The end of the tile GEMV, after the row sums (sc.redR) and the 16-lane
+// column partials (sc.redC) of every block are in LDS: y in the fixed order
+// redR + ((C0 + C1) + (C2 + C3)) over the column partials, the folded
+// diagonals and, user side, the bias column / row.
+template <int NB, bool USER>
+__device__ __forceinline__ void tile_matvec_finish(MvScratch<NB>& sc, double vb,
+                                                   const float* __restrict__ Gs_e, float gn, int k,
+                                                   double (&yo)[(16 * NB + 63) / 64], double& yb) {
+  constexpr int NF = NB / 2, NP = 16 * NB, NV = (NP + 63) / 64;
+  const int lane = threadIdx.x & 63;
   __builtin_amdgcn_wave_barrier();
   double ybp = 0.0;
 #pragma unroll
@@ -393,6 +411,140 @@ __device__ __forceinline__ void tile_matvec(
     yo[h] = y;
   }
   if (USER) yb = fma((double)gn, vb, wave_sum_f64(ybp));
+}
+
+// Streamed tile GEMV for NB > 4 (k = 65 ... 128): the same products, sums and
+// order as tile_matvec, in ONE pass over the tiles instead of two passes over
+// tiles held in registers (32 tiles = 128 VGPRs at k = 128: with the column
+// partials and the CG vectors both the matvec and the one-pass kernel spilled).
+// The tiles are consumed in block-row order -- row bi's strictly-upper tiles
+// (bi, bj > bi), then its diagonal tile -- and each tile feeds both of its
+// sums: the row sum of bi (T v_bj, summed over bj ascending and the diagonal
+// last, as pass 1) and the column partials of bj (T^T v_bi, summed over bi
+// ascending with bj's own diagonal last, as pass 2: every (bi < bj) tile of
+// column bj precedes row bj's diagonal in this order).  Row bi's sum and
+// column bi's partials are complete after row bi's diagonal and go to LDS
+// there, so the live column accumulators shrink row by row.  Loads run
+// TD tiles ahead of the tile being multiplied through a register ring:
+// ring[] holds the stream's first TD tiles on entry (tile_stream_load), the
+// rest are loaded from Ge (this lane's float4 of tile t at Ge[64 t + lane]).
+template <int NB>
+struct TileStream {   // load order: t[i] = tile index of the i-th tile consumed
+  static constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2, NTILE = NO + NF + (NB & 1);
+  int t[NTILE];
+  constexpr TileStream() : t() {
+    int n = 0;
+    for (int bi = 0; bi < NB; ++bi) {
+      for (int bj = bi + 1; bj < NB; ++bj) t[n++] = bi * NB - bi * (bi + 1) / 2 + (bj - bi - 1);
+      if ((bi & 1) == 0) t[n++] = bi < 2 * NF ? NO + bi / 2 : NO + NF;   // odd rows reuse it
+    }
+  }
+};
+// load position of tile (bi, bj > bi) / of row bi's diagonal tile (even bi)
+__host__ __device__ constexpr int stream_pos_off(int bi, int bj, int nb) {
+  return bi * nb - bi * (bi + 1) / 2 + (bj - bi - 1) + (bi + 1) / 2;
+}
+__host__ __device__ constexpr int stream_pos_diag(int bi, int nb) {
+  return bi * nb - bi * (bi + 1) / 2 + (nb - 1 - bi) + (bi + 1) / 2;
+}
+template <int NB>
+constexpr bool tile_stream_consistent() {
+  constexpr TileStream<NB> S{};
+  for (int bi = 0; bi < NB; ++bi) {
+    for (int bj = bi + 1; bj < NB; ++bj)
+      if (S.t[stream_pos_off(bi, bj, NB)] != bi * NB - bi * (bi + 1) / 2 + (bj - bi - 1)) return false;
+    if ((bi & 1) == 0 &&
+        S.t[stream_pos_diag(bi, NB)] != (bi < 2 * (NB / 2) ? NB * (NB - 1) / 2 + bi / 2
+                                                            : NB * (NB - 1) / 2 + NB / 2))
+      return false;
+  }
+  return true;
+}
+static_assert(tile_stream_consistent<5>() && tile_stream_consistent<6>() &&
+                  tile_stream_consistent<7>() && tile_stream_consistent<8>(),
+              "stream positions disagree with the load order");
+// NB > 4 streams its tiles (MR_TS_STREAM 0: the two-pass register form)
+#ifndef MR_TS_STREAM
+#define MR_TS_STREAM 1
+#endif
+#ifndef MR_TS_AHEAD
+#define MR_TS_AHEAD 12
+#endif
+template <int NB>
+constexpr int ts_ahead() {
+  constexpr int n = NB * (NB - 1) / 2 + NB / 2 + (NB & 1);
+  return MR_TS_AHEAD < n ? MR_TS_AHEAD : n;
+}
+template <bool NT>
+__device__ __forceinline__ float4 tile_ld(const floatx4* __restrict__ Ge, int t, int lane) {
+  const floatx4 v = NT ? __builtin_nontemporal_load(Ge + t * 64 + lane) : Ge[t * 64 + lane];
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+template <int NB, bool NT>
+__device__ __forceinline__ void tile_stream_load(const floatx4* __restrict__ Ge, int lane,
+                                                 float4 (&ring)[ts_ahead<NB>()]) {
+  constexpr TileStream<NB> S{};
+#pragma unroll
+  for (int i = 0; i < ts_ahead<NB>(); ++i) ring[i] = tile_ld<NT>(Ge, S.t[i], lane);
+}
+template <int NB, bool USER, bool NT>
+__device__ __forceinline__ void tile_matvec_stream(
+    const floatx4* __restrict__ Ge, float4 (&ring)[ts_ahead<NB>()], MvScratch<NB>& sc, double vb,
+    const float* __restrict__ Gs_e, float gn, int k, double (&yo)[(16 * NB + 63) / 64],
+    double& yb) {
+  constexpr TileStream<NB> S{};
+  constexpr int NTILE = TileStream<NB>::NTILE, NF = NB / 2, TD = ts_ahead<NB>();
+  const int lane = threadIdx.x & 63;
+  const int rr = lane >> 2, c4 = (lane & 3) * 4;
+  // take the tile at load position i and refill its ring slot with i + TD
+  auto take = [&](int i, double (&ge)[4]) {
+    float4 gg = ring[i % TD];
+    if (i + TD < NTILE) ring[i % TD] = tile_ld<NT>(Ge, S.t[i + TD], lane);
+    ge[0] = gg.x; ge[1] = gg.y; ge[2] = gg.z; ge[3] = gg.w;
+  };
+  double cc[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) cc[b][0] = cc[b][1] = cc[b][2] = cc[b][3] = 0.0;
+  double dge[4] = {0.0, 0.0, 0.0, 0.0};   // the folded diagonal tile, kept for the odd row
+#pragma unroll
+  for (int bi = 0; bi < NB; ++bi) {
+    double s0 = 0.0;
+    const double pi = sc.pv[16 * bi + rr];
+#pragma unroll
+    for (int bj = bi + 1; bj < NB; ++bj) {
+      double ge[4];
+      take(stream_pos_off(bi, bj, NB), ge);
+#pragma unroll
+      for (int x = 0; x < 4; ++x) s0 = fma(ge[x], sc.pv[16 * bj + c4 + x], s0);
+#pragma unroll
+      for (int x = 0; x < 4; ++x) cc[bj][x] = fma(ge[x], pi, cc[bj][x]);
+      // the products happen here, not where their sums are next needed (the
+      // compiler otherwise sinks them and keeps the tiles' fp64 copies live)
+      asm volatile("" : "+v"(s0), "+v"(cc[bj][0]), "+v"(cc[bj][1]), "+v"(cc[bj][2]), "+v"(cc[bj][3]));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if ((bi & 1) == 0) take(stream_pos_diag(bi, NB), dge);
+    const bool lower = (bi & 1) && bi < 2 * NF;
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const int c = c4 + x;
+      const bool use = lower ? (c < rr) : (c >= rr);   // lower: diagonal from dd
+      s0 = fma(use ? dge[x] : 0.0, sc.pv[16 * bi + c], s0);
+    }
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const int c = c4 + x;
+      const bool use = lower ? (c < rr) : (c > rr);
+      cc[bi][x] = fma(use ? dge[x] : 0.0, pi, cc[bi][x]);
+    }
+    const double rs = quad_sum_f64(s0);
+    if ((lane & 3) == 0) sc.redR[bi][rr] = rs;
+    double2* dst = reinterpret_cast<double2*>(&sc.redC[bi][4 * lane]);
+    dst[0] = make_double2(cc[bi][0], cc[bi][1]);
+    dst[1] = make_double2(cc[bi][2], cc[bi][3]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  tile_matvec_finish<NB, USER>(sc, vb, Gs_e, gn, k, yo, yb);
 }
 
 // CG start for ONE entity, by one wave, in block form (cg_least_squares,
@@ -2135,6 +2287,7 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 4 : 2)) void cg_matvec_kernel(
   constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2, NTILE = NO + NF + (NB & 1);
   constexpr int64_t GS = (int64_t)NTILE * 256 + NF * 16;   // == gsize_of(k)
   constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
+  constexpr bool STREAM = MR_TS_STREAM && NB > 4;
   __shared__ MvScratch<NB> scr[MV_WAVES];
   __shared__ double sh[MV_WAVES];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -2158,11 +2311,12 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 4 : 2)) void cg_matvec_kernel(
       if (update_p) rbias = rb[e];
     }
     const floatx4* __restrict__ Ge = reinterpret_cast<const floatx4*>(G + e * GS);
-    float4 g[NTILE];
+    float4 g[STREAM ? ts_ahead<NB>() : NTILE];
+    if constexpr (STREAM) {
+      tile_stream_load<NB, true>(Ge, lane, g);
+    } else {
 #pragma unroll
-    for (int t = 0; t < NTILE; ++t) {
-      const floatx4 x = __builtin_nontemporal_load(Ge + t * 64 + lane);
-      g[t] = make_float4(x[0], x[1], x[2], x[3]);
+      for (int t = 0; t < NTILE; ++t) g[t] = tile_ld<true>(Ge, t, lane);
     }
     float d2 = 0.f;   // diagonal of the odd diagonal blocks (side array)
     if (NF > 0 && lane < 16 * NF) d2 = G[e * GS + NTILE * 256 + lane];
@@ -2186,8 +2340,12 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 4 : 2)) void cg_matvec_kernel(
     if (NF > 0 && lane < 16 * NF) sc.dd[lane] = d2;
     __builtin_amdgcn_wave_barrier();
     double yo[NV], ybv = 0.0;
-    tile_matvec<NB, USER>(g, sc, vbias, USER ? Gs + e * ldk : nullptr, USER ? Gn[e] : 0.f, k,
-                          yo, ybv);
+    if constexpr (STREAM)
+      tile_matvec_stream<NB, USER, true>(Ge, g, sc, vbias, USER ? Gs + e * ldk : nullptr,
+                                         USER ? Gn[e] : 0.f, k, yo, ybv);
+    else
+      tile_matvec<NB, USER>(g, sc, vbias, USER ? Gs + e * ldk : nullptr, USER ? Gn[e] : 0.f, k,
+                            yo, ybv);
     double d = 0.0;
 #pragma unroll
     for (int h = 0; h < NV; ++h) {
@@ -2253,14 +2411,8 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 4 : 2)) void cg_matvec_kernel(
 // stream is far larger than the Infinity Cache: nothing of it survives to the
 // next sweep) or with the default policy (a shard small enough to stay
 // on-die between sweeps); the engine picks per side (Engine::tile_nt_for)
-#ifndef MR_OP_LOOKAHEAD   // entity e + 1's operands loaded while e is processed (NB <= 4)
-#define MR_OP_LOOKAHEAD 0
-#endif
-#ifndef MR_OP_LA_WAVES    // waves per SIMD the lookahead form is bounded to
-#define MR_OP_LA_WAVES 3
-#endif
-template <int NB, bool USER, bool NT, bool LA = (MR_OP_LOOKAHEAD != 0 && NB <= 4)>
-__global__ __launch_bounds__(256, (NB <= 4 ? (LA ? MR_OP_LA_WAVES : (USER && NB == 4 ? MR_OP_WAVES_U4 : MR_OP_WAVES)) : 2))
+template <int NB, bool USER, bool NT>
+__global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 : MR_OP_WAVES) : 2))
 #ifdef MR_OP_WPE
 __attribute__((amdgpu_waves_per_eu(MR_OP_WPE, MR_OP_WPE)))
 #endif
@@ -2277,6 +2429,8 @@ void cg_onepass_kernel(
   constexpr int64_t GS = (int64_t)NTILE * 256 + NF * 16;   // == gsize_of(k)
   constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
   constexpr int XC = xchunk_of(NB, USER);
+  constexpr bool STREAM = MR_TS_STREAM && NB > 4;
+  constexpr int NHELD = STREAM ? ts_ahead<NB>() : NTILE;   // tiles held per entity
   __shared__ MvScratch<NB> scr[MV_WAVES];
   __shared__ double rvs[MV_WAVES][16 * NB];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -2304,16 +2458,16 @@ void cg_onepass_kernel(
     double a = 0.0, b = 0.0, c = 0.0;
     double d = 0.0;   // r.r of the updated residual (matrix.cpp:507's direct dot)
     // One entity's operands: the CG vectors' entries of this lane, the bias
-    // entries (user side) and the G tiles.  MR_OP_LOOKAHEAD: entity e + 1's
-    // are loaded while entity e is updated and multiplied (one more register
-    // set), so a wave that owns few entities -- a shard of an N-GPU run --
-    // does not pay a full memory latency per entity; same values, same order.
+    // entries (user side) and the G tiles (NB > 4: the first tiles of the
+    // stream, tile_matvec_stream loads the rest).  Loading entity e + 1's
+    // while e is processed (one more register set) measured 6 % (full size)
+    // to 17 % (an 8-rank shard) slower per CG iteration at k = 64: not kept.
     struct Ent {
       double pi[NV], ri[NV], qi[NV];
       float xi[NV];
       double pbias, rbias, qbias;
       float xbias, d2;
-      float4 g[NTILE];
+      float4 g[NHELD];
     };
     auto load_ent = [&](int64_t e, Ent& E_) {
       const double* pe = p + e * ldk;
@@ -2339,15 +2493,16 @@ void cg_onepass_kernel(
         }
       }
       const floatx4* __restrict__ Ge = reinterpret_cast<const floatx4*>(G + e * GS);
+      if constexpr (STREAM) {
+        tile_stream_load<NB, NT>(Ge, lane, E_.g);
+      } else {
 #pragma unroll
-      for (int t = 0; t < NTILE; ++t) {
-        const floatx4 v4 = NT ? __builtin_nontemporal_load(Ge + t * 64 + lane) : Ge[t * 64 + lane];
-        E_.g[t] = make_float4(v4[0], v4[1], v4[2], v4[3]);
+        for (int t = 0; t < NTILE; ++t) E_.g[t] = tile_ld<NT>(Ge, t, lane);
       }
       E_.d2 = 0.f;
       if (NF > 0 && lane < 16 * NF) E_.d2 = G[e * GS + NTILE * 256 + lane];
     };
-    auto process = [&](int64_t e, const Ent& E_) {
+    auto process = [&](int64_t e, Ent& E_) {
       double* pe = p + e * ldk;
       double* re = r + e * ldk;
       double* qe = q + e * ldk;
@@ -2385,8 +2540,13 @@ void cg_onepass_kernel(
       if (NF > 0 && lane < 16 * NF) sc.dd[lane] = E_.d2;
       __builtin_amdgcn_wave_barrier();
       double yo[NV], ybv = 0.0;
-      tile_matvec<NB, USER, (NB > 4) || MR_OP_OPAQUE>(E_.g, sc, pbias, USER ? Gs + e * ldk : nullptr,
-                                                      USER ? Gn[e] : 0.f, k, yo, ybv);
+      if constexpr (STREAM)
+        tile_matvec_stream<NB, USER, NT>(reinterpret_cast<const floatx4*>(G + e * GS), E_.g, sc,
+                                         pbias, USER ? Gs + e * ldk : nullptr, USER ? Gn[e] : 0.f,
+                                         k, yo, ybv);
+      else
+        tile_matvec<NB, USER, (NB > 4) || MR_OP_OPAQUE>(E_.g, sc, pbias, USER ? Gs + e * ldk : nullptr,
+                                                        USER ? Gn[e] : 0.f, k, yo, ybv);
 #pragma unroll
       for (int h = 0; h < NV; ++h) {
         const int o = lane + 64 * h;
@@ -2408,20 +2568,10 @@ void cg_onepass_kernel(
       }
       __builtin_amdgcn_wave_barrier();
     };
-    if constexpr (LA) {
-      Ent cur, nxt;
-      load_ent(c0, cur);
-      for (int64_t e = c0; e < c1; ++e) {
-        if (e + 1 < c1) load_ent(e + 1, nxt);
-        process(e, cur);
-        cur = nxt;
-      }
-    } else {
-      for (int64_t e = c0; e < c1; ++e) {
-        Ent cur;
-        load_ent(e, cur);
-        process(e, cur);
-      }
+    for (int64_t e = c0; e < c1; ++e) {
+      Ent cur;
+      load_ent(e, cur);
+      process(e, cur);
     }
     a = wave_sum_f64(a);
     b = wave_sum_f64(b);
@@ -3301,9 +3451,6 @@ constexpr int SP_THREADS = 256;
 #define MR_SP_AUX 0
 #endif
 constexpr int SP_TILE = kSpTile;     // staged products per row block (16 KiB fp64)
-#ifndef MR_SP_GPRE   // gathers of the next short block issued before this block's row sums
-#define MR_SP_GPRE 0
-#endif
 
 template <int GATHER, int OUT, bool BUF>
 __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
@@ -3427,11 +3574,6 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
     }
     if (n1 - n0 <= SP_TILE) load_short(cur, r0, r1, n0, n1);
   }
-  // MR_SP_GPRE: the next short block's gathers (its ids arrived with
-  // load_short) are issued behind this block's product stores, so they are
-  // in flight during the barrier and the row sums (same values, same order)
-  double gpre[MR_SP_GPRE ? PER : 1];
-  bool have_pre = false;
   for (; b < n_blk; b += gs) {
     const bool has_next = b + gs < n_blk, has_next2 = b + 2 * gs < n_blk;
     const bool next_short = has_next && qn1 - qn0 <= SP_TILE;
@@ -3443,25 +3585,13 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
     }
     if (n1 - n0 <= SP_TILE) {
       double gx[PER];
-      if (MR_SP_GPRE && have_pre) {
 #pragma unroll
-        for (int u = 0; u < PER; ++u) gx[u] = gpre[u];
-      } else {
-#pragma unroll
-        for (int u = 0; u < PER; ++u) gx[u] = gather(cur.cc[u]);
-      }
+      for (int u = 0; u < PER; ++u) gx[u] = gather(cur.cc[u]);
       const int nl = (int)(n1 - n0);
 #pragma unroll
       for (int u = 0; u < PER; ++u) {
         const int jl = BUF ? 8 * t + u : t + u * SP_THREADS;   // load_short's entry map
         if (jl < nl) prod[jl] = cur.vv[u] * gx[u];
-      }
-      if (MR_SP_GPRE) {
-        have_pre = next_short;
-        if (next_short) {
-#pragma unroll
-          for (int u = 0; u < PER; ++u) gpre[u] = gather(nxt.cc[u]);
-        }
       }
       const int R = (int)(r1 - r0);
       if (t < R) srp[t] = cur.rpo;
@@ -3490,7 +3620,6 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
       if (lr < R && g == 0) emit(r0 + lr, sum);
       __syncthreads();   // prod / srp are reused by the next block
     } else {             // one long row: per-thread strided sums, fixed-order tree
-      if (MR_SP_GPRE) have_pre = false;
       double sum = 0.0;
       for (int64_t j = n0 + t; j < n1; j += SP_THREADS) sum += v[j] * gather(ci[j]);
       sum = block_sum_f64<SP_THREADS>(sum, sh);
