@@ -12,6 +12,7 @@
 #   ab=ARGS             python tools/cg_ab.py ARGS -> ab_<i>.jsonl (fixed CG counts)
 #   stats=ARGS          rocprofv3 --kernel-trace --stats over bench.py ARGS
 #   pmc=CTRS@ARGS       rocprofv3 --pmc CTRS (space-separated) over bench.py ARGS
+#   ktrace=SCRIPT ARGS  rocprofv3 --kernel-trace over python SCRIPT ARGS (tools/trace_gaps.py)
 #   py=SCRIPT ARGS      python SCRIPT ARGS         -> py_<i>.log
 #   setenv=VAR=VALUE    export VAR for the following steps (e.g. MR_LIB_PATH=...)
 #   unsetenv=VAR        unset it
@@ -54,6 +55,10 @@ for step in "$@"; do
         python3 bench.py $arg > $OUT/stats_$i.json 2> $OUT/stats_$i.err
       rc=$?; find $OUT/stats_$i -name "*kernel_stats.csv" | head -3
       [ $rc -ne 0 ] && stop stats $rc ;;
+    ktrace)
+      timeout -k 10 600 rocprofv3 --kernel-trace -d $OUT/ktrace_$i -o run -- \
+        python3 $arg > $OUT/ktrace_$i.log 2>&1
+      rc=$?; tail -3 $OUT/ktrace_$i.log; [ $rc -ne 0 ] && stop ktrace $rc ;;
     pmc)
       ctrs=${arg%%@*}; bargs=${arg#*@}
       timeout -s KILL 300 rocprofv3 --pmc $ctrs -d $OUT/pmc_$i -o run -- \
