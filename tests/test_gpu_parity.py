@@ -302,13 +302,15 @@ def test_gram_kernel_vs_numpy(gpu, k, ratings):
     _lib.check(_lib.lib().mr_set_gram_chunk(2048), "reset chunk")
 
 
-@pytest.mark.parametrize("k", [5, 10, 32, 33, 64, 65, 128, 144, 200, 300])
+@pytest.mark.parametrize("k", [5, 10, 32, 33, 64, 65, 96, 112, 128, 144, 200, 300])
 @pytest.mark.parametrize("fuse,chunk,onepass", [(1, 2048, 1), (1, 64, 1), (0, 2048, 1),
                                                 (1, 2048, 0), (0, 2048, 0)])
 def test_cg_iterations_vs_oracle(gpu, k, fuse, chunk, onepass):
     """The first CG iterations of both sides -- CG start (fused in the Gram
     epilogue, after slab_reduce for split entities, or the unfused matvec +
-    INIT update), the NB = 1..8 block GEMV, the update and the fused control
+    INIT update), the NB = 1..8 block GEMV (NB = 5..8: the streamed tiles of
+    tile_matvec_stream, odd NB with an unfolded last diagonal block), the
+    update and the fused control
     -- against the oracle's fp64 CG (matrix.cpp:456-529 in block form) run on
     the GPU's own normal equations (fp32 values read back).  What remains is
     summation order (and, one-pass, r'.r' from r.r + 2 alpha r.q + alpha^2
