@@ -317,6 +317,14 @@ int mr_als_set_option(mr_als* ctx, int option, double value) {
   }
 }
 
+// Diagnostics (tools/op_timeline.py; not part of the reference ABI): the
+// s_memrealtime timeline of the last one-pass CG launch in an MR_OP_PROF
+// build (returns the number of values copied, 0 in a product build).
+int mr_debug_op_timeline(long long* out, int n) {
+  MR_CHECK(out && n > 0, "bad buffer");
+  return mr::op_prof_read(reinterpret_cast<int64_t*>(out), n);
+}
+
 int mr_set_gram_chunk(int chunk) {
   MR_CHECK(chunk >= 64 && chunk <= (1 << 30), "chunk must be in [64, 2^30]");
   g_gram_chunk = chunk;

@@ -2411,6 +2411,23 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 4 : 2)) void cg_matvec_kernel(
 // stream is far larger than the Infinity Cache: nothing of it survives to the
 // next sweep) or with the default policy (a shard small enough to stay
 // on-die between sweeps); the engine picks per side (Engine::tile_nt_for)
+// Diagnostic timeline of the one-pass kernel (MR_OP_PROF builds only,
+// tools/op_timeline.py): per block, s_memrealtime (100 MHz) at entry, after
+// its entities, after its bin flush; the last block also after the bin
+// collection, after the state update and after the publish.
+#ifndef MR_OP_PROF
+#define MR_OP_PROF 0
+#endif
+constexpr int kOpProfBlocks = 4096;
+__device__ int64_t g_op_prof[8 + 4 * kOpProfBlocks];
+__device__ __forceinline__ void op_prof(int slot) {
+  if constexpr (MR_OP_PROF) {
+    const int64_t t = (int64_t)__builtin_amdgcn_s_memrealtime();
+    if (slot < 8) g_op_prof[slot] = t;
+    else if (blockIdx.x < kOpProfBlocks) g_op_prof[8 + 4 * blockIdx.x + (slot - 8)] = t;
+  }
+}
+
 template <int NB, bool USER, bool NT>
 __global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 : MR_OP_WAVES) : 2))
 #ifdef MR_OP_WPE
@@ -2424,6 +2441,7 @@ void cg_onepass_kernel(
     float* __restrict__ x, float* __restrict__ xb, int64_t* __restrict__ xbins,
     CgMirror* mirror, int seq) {
   if (ald(&st->done)) return;
+  if (threadIdx.x == 0) op_prof(8);
   const double beta = ald(&st->beta), alpha = ald(&st->alpha);
   constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2, NTILE = NO + NF + (NB & 1);
   constexpr int64_t GS = (int64_t)NTILE * 256 + NF * 16;   // == gsize_of(k)
@@ -2584,6 +2602,7 @@ void cg_onepass_kernel(
       atomicAdd((unsigned long long*)&xacc[0][3][lane], (unsigned long long)xterm(d, lane));
     }
   }
+  if (threadIdx.x == 0) op_prof(9);
   xsum_flush_lds<4>(xacc, xbins, 1);
   // last-arriving block: iteration t's scalars (see last_block_finalize for
   // the memory-model basis of this hand-off; the bins' atomics are drained
@@ -2591,13 +2610,16 @@ void cg_onepass_kernel(
   __shared__ int s_last;
   if (threadIdx.x == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    op_prof(10);
     s_last = __hip_atomic_fetch_add(&st->arrive, 1u, __ATOMIC_RELAXED,
                                     __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   }
   __syncthreads();
   if (!s_last || wid != 0) return;
   __shared__ int64_t xs[4 * kXW];
+  if (lane == 0) op_prof(0);
   int64_t tot = xsum_collect<4>(xbins, lane);
+  if (lane == 0) op_prof(1);
   if (lane == 0) __hip_atomic_store(&st->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (PeerComm* pc = ald(&st->peer)) {
     if (!peer_sum_lanes(pc, tot, 4 * kXW)) {
@@ -2623,8 +2645,18 @@ void cg_onepass_kernel(
     apply_beta(v, fma(al * al, sum[2], fma(2.0 * al, sum[1], v.rr)));
     store_state(st, v);
     ast(&st->pending, 1);
+    op_prof(2);
     publish(v, mirror, seq);
+    op_prof(3);
   }
+}
+
+// MR_OP_PROF builds: copy the last one-pass launch's timeline out (slots 0-3:
+// the last block; then 4 per block: entry, entities done, flushed, unused)
+int op_prof_read(int64_t* out, int n) {
+  n = n < 8 + 4 * kOpProfBlocks ? n : 8 + 4 * kOpProfBlocks;
+  MR_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_op_prof), (size_t)n * sizeof(int64_t)));
+  return MR_OP_PROF ? n : 0;
 }
 
 int onepass_blocks_per_cu(bool user_side, int k) {

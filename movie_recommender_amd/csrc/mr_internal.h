@@ -300,6 +300,8 @@ int launch_cg_matvec(hipStream_t s, bool user_side, const CgState* st,
 // Blocks of cg_onepass_kernel one CU holds at once for this side and k (0:
 // unknown); the one-pass grid is that times the CU count.
 int onepass_blocks_per_cu(bool user_side, int k);
+// diagnostic timeline of the last one-pass launch (MR_OP_PROF builds; 0 otherwise)
+int op_prof_read(int64_t* out, int n);
 int launch_cg_onepass(hipStream_t s, bool user_side, CgState* st, int update, int rev, int64_t E, int k,
                       const float* G, const float* Gs, const float* Gn, double* p, double* pb,
                       double* r, double* rb, double* q, double* qb, float* x, float* xb,
