@@ -2428,8 +2428,16 @@ __device__ __forceinline__ void op_prof(int slot) {
   }
 }
 
-template <int NB, bool USER, bool NT>
-__global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 : MR_OP_WAVES) : 2))
+// MR_OP_PP (NB <= 4): the next entity's operands are loaded while the
+// current one is processed (two register sets, MR_OP_PP_WAVES waves / SIMD)
+#ifndef MR_OP_PP
+#define MR_OP_PP 0
+#endif
+#ifndef MR_OP_PP_WAVES
+#define MR_OP_PP_WAVES 3
+#endif
+template <int NB, bool USER, bool NT, bool PP = (MR_OP_PP != 0 && NB <= 4)>
+__global__ __launch_bounds__(256, (NB <= 4 ? (PP ? MR_OP_PP_WAVES : (USER && NB == 4 ? MR_OP_WAVES_U4 : MR_OP_WAVES)) : 2))
 #ifdef MR_OP_WPE
 __attribute__((amdgpu_waves_per_eu(MR_OP_WPE, MR_OP_WPE)))
 #endif
@@ -2586,10 +2594,27 @@ void cg_onepass_kernel(
       }
       __builtin_amdgcn_wave_barrier();
     };
-    for (int64_t e = c0; e < c1; ++e) {
-      Ent cur;
-      load_ent(e, cur);
-      process(e, cur);
+    if constexpr (PP) {
+      // two operand sets in alternation (no copy between them: a copy would
+      // wait for the next entity's loads), so entity e + 1's loads are in
+      // flight while e is updated and multiplied
+      Ent A, B;
+      int64_t e = c0;
+      load_ent(e, A);
+      while (true) {
+        if (e + 1 < c1) load_ent(e + 1, B);
+        process(e, A);
+        if (++e >= c1) break;
+        if (e + 1 < c1) load_ent(e + 1, A);
+        process(e, B);
+        if (++e >= c1) break;
+      }
+    } else {
+      for (int64_t e = c0; e < c1; ++e) {
+        Ent cur;
+        load_ent(e, cur);
+        process(e, cur);
+      }
     }
     a = wave_sum_f64(a);
     b = wave_sum_f64(b);
@@ -2617,11 +2642,17 @@ void cg_onepass_kernel(
   __syncthreads();
   if (!s_last || wid != 0) return;
   __shared__ int64_t xs[4 * kXW];
+  __shared__ double xv[4];
   if (lane == 0) op_prof(0);
+  // the state and the peer pointer are loaded before the bins, so their
+  // latency overlaps the collection (the serial tail of every iteration)
+  PeerComm* pc = ald(&st->peer);
+  CgScalars v{};
+  if (lane == 0) v = load_state(st);
   int64_t tot = xsum_collect<4>(xbins, lane);
   if (lane == 0) op_prof(1);
   if (lane == 0) __hip_atomic_store(&st->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (PeerComm* pc = ald(&st->peer)) {
+  if (pc) {
     if (!peer_sum_lanes(pc, tot, 4 * kXW)) {
       if (lane == 0) peer_fail(st, mirror, seq);
       return;
@@ -2629,11 +2660,12 @@ void cg_onepass_kernel(
   }
   if (lane < 4 * kXW) xs[lane] = tot;
   __builtin_amdgcn_wave_barrier();
+  if (lane < 4) xv[lane] = xsum_value(&xs[lane * kXW]);   // the four sums in parallel
+  __builtin_amdgcn_wave_barrier();
   if (lane == 0) {
     double sum[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) sum[j] = xsum_value(&xs[j * kXW]);
-    CgScalars v = load_state(st);
+    for (int j = 0; j < 4; ++j) sum[j] = xv[j];
     // iteration t >= 1: alpha and the next r'.r' start from the DIRECT r.r of
     // the residual just updated, not from the previous kernel's derived value,
     // so the derivation's rounding does not accumulate across iterations
