@@ -2428,16 +2428,8 @@ __device__ __forceinline__ void op_prof(int slot) {
   }
 }
 
-// MR_OP_PP (NB <= 4): the next entity's operands are loaded while the
-// current one is processed (two register sets, MR_OP_PP_WAVES waves / SIMD)
-#ifndef MR_OP_PP
-#define MR_OP_PP 0
-#endif
-#ifndef MR_OP_PP_WAVES
-#define MR_OP_PP_WAVES 3
-#endif
-template <int NB, bool USER, bool NT, bool PP = (MR_OP_PP != 0 && NB <= 4)>
-__global__ __launch_bounds__(256, (NB <= 4 ? (PP ? MR_OP_PP_WAVES : (USER && NB == 4 ? MR_OP_WAVES_U4 : MR_OP_WAVES)) : 2))
+template <int NB, bool USER, bool NT>
+__global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 : MR_OP_WAVES) : 2))
 #ifdef MR_OP_WPE
 __attribute__((amdgpu_waves_per_eu(MR_OP_WPE, MR_OP_WPE)))
 #endif
@@ -2486,8 +2478,9 @@ void cg_onepass_kernel(
     // One entity's operands: the CG vectors' entries of this lane, the bias
     // entries (user side) and the G tiles (NB > 4: the first tiles of the
     // stream, tile_matvec_stream loads the rest).  Loading entity e + 1's
-    // while e is processed (one more register set) measured 6 % (full size)
-    // to 17 % (an 8-rank shard) slower per CG iteration at k = 64: not kept.
+    // while e is processed (a second register set used in alternation, 2 or
+    // 3 waves / SIMD) measured 14-32 % (an 8-rank shard) and 19-33 % (full
+    // size) slower per users CG iteration at k = 64 (profiles/r04/r04l).
     struct Ent {
       double pi[NV], ri[NV], qi[NV];
       float xi[NV];
@@ -2594,27 +2587,10 @@ void cg_onepass_kernel(
       }
       __builtin_amdgcn_wave_barrier();
     };
-    if constexpr (PP) {
-      // two operand sets in alternation (no copy between them: a copy would
-      // wait for the next entity's loads), so entity e + 1's loads are in
-      // flight while e is updated and multiplied
-      Ent A, B;
-      int64_t e = c0;
-      load_ent(e, A);
-      while (true) {
-        if (e + 1 < c1) load_ent(e + 1, B);
-        process(e, A);
-        if (++e >= c1) break;
-        if (e + 1 < c1) load_ent(e + 1, A);
-        process(e, B);
-        if (++e >= c1) break;
-      }
-    } else {
-      for (int64_t e = c0; e < c1; ++e) {
-        Ent cur;
-        load_ent(e, cur);
-        process(e, cur);
-      }
+    for (int64_t e = c0; e < c1; ++e) {
+      Ent cur;
+      load_ent(e, cur);
+      process(e, cur);
     }
     a = wave_sum_f64(a);
     b = wave_sum_f64(b);
