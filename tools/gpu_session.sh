@@ -51,7 +51,7 @@ for step in "$@"; do
       timeout -k 10 600 python -u tools/cg_ab.py $arg >> $OUT/ab_$i.jsonl 2> $OUT/ab_$i.err
       rc=$?; tail -c 800 $OUT/ab_$i.jsonl; [ $rc -ne 0 ] && stop ab $rc ;;
     stats)
-      timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/stats_$i -o run -- \
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats -f csv rocpd -d $OUT/stats_$i -o run -- \
         python3 bench.py $arg > $OUT/stats_$i.json 2> $OUT/stats_$i.err
       rc=$?; find $OUT/stats_$i -name "*kernel_stats.csv" | head -3
       [ $rc -ne 0 ] && stop stats $rc ;;
@@ -61,7 +61,7 @@ for step in "$@"; do
       rc=$?; tail -3 $OUT/ktrace_$i.log; [ $rc -ne 0 ] && stop ktrace $rc ;;
     pmc)
       ctrs=${arg%%@*}; bargs=${arg#*@}
-      timeout -s KILL 300 rocprofv3 --pmc $ctrs -d $OUT/pmc_$i -o run -- \
+      timeout -s KILL 300 rocprofv3 --pmc $ctrs -f csv -d $OUT/pmc_$i -o run -- \
         python3 bench.py $bargs > $OUT/pmc_$i.json 2> $OUT/pmc_$i.err
       rc=$?; [ $rc -ne 0 ] && stop pmc $rc ;;
     py)
