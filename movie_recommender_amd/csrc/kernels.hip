@@ -14,7 +14,6 @@
 //   solve_kernel     exact per-entity Cholesky (north-star "exact" mode)
 // Wave = 64 lanes throughout; no CUDA idioms.
 #include <cstdlib>
-#include <type_traits>
 #include <utility>
 
 #include "mr_internal.h"
