@@ -78,9 +78,6 @@ __device__ T block_sum_t(T v, T* sh) {
 // broadcasts; candidate rows are staged 16 factors at a time.
 // ---------------------------------------------------------------------------
 constexpr int SC_U = 32, SC_C = 256, SC_KC = 16;
-#ifndef MR_SC_NT_KEYS   // non-temporal stores of the score keys (read back only by the select)
-#define MR_SC_NT_KEYS 0
-#endif
 
 template <bool KEYS>
 __global__ __launch_bounds__(256) void rec_score_kernel(
@@ -174,9 +171,7 @@ __global__ __launch_bounds__(256) void rec_score_kernel(
       const double s = add_rn(add_rn(acc[p][q], bias), med[c]);
       if constexpr (KEYS) {
         const uint64_t key = score_key(s);
-        uint64_t* dst = reinterpret_cast<uint64_t*>(out) + (int64_t)u * ld + c;
-        if constexpr (MR_SC_NT_KEYS) __builtin_nontemporal_store(key, dst);
-        else *dst = key;
+        reinterpret_cast<uint64_t*>(out)[(int64_t)u * ld + c] = key;
         lo = min(lo, (unsigned long long)key);
         hi = max(hi, (unsigned long long)key);
       } else {

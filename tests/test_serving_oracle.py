@@ -91,66 +91,3 @@ def test_exclusion_csr_matches_container_path():
     with pytest.raises(ValueError):
         t._exclusions_csr(off[:-1], ids, len(lists))
 
-
-def _key64(s):
-    """The order-preserving 64-bit key of serving.hip score_key (-0.0 -> +0.0)."""
-    s = np.where(s == 0.0, 0.0, s)
-    b = s.view(np.uint64)
-    neg = (b >> np.uint64(63)) == 1
-    return np.where(neg, ~b, b | np.uint64(1 << 63))
-
-
-def _key_score(key):
-    neg = (key >> np.uint64(63)) == 0
-    b = np.where(neg, ~key, key & np.uint64(0x7FFFFFFFFFFFFFFF))
-    return b.view(np.float64)
-
-
-def _truncated_select(s, mids, excl, N, bins=2048, cap=2048):
-    """The select of rec_select_kernel's fast path on truncated keys: bins of
-    the decoded top-32-bit keys over the exact [min, max], the boundary bin of
-    the N-th largest, the candidates at or above it re-ranked by their exact
-    (score, movie id).  Returns None where the kernel takes its radix path."""
-    key = _key64(s)
-    t = (key >> np.uint64(32)).astype(np.uint64)
-    t[excl] = 0
-    live = t != 0
-    kmin, kmax = key[live].min(), key[live].max()
-    smin, smax = _key_score(np.array([kmin]))[0], _key_score(np.array([kmax]))[0]
-    if not smax > smin:
-        return None
-    scale = bins / (smax - smin)
-    v = np.where(live, (_key_score(t << np.uint64(32)) - smin) * scale, 0.0)  # t = 0: excluded
-    b = np.minimum(bins - 1, np.floor(np.maximum(v, 0.0)).astype(np.int64))
-    hist = np.bincount(b[live], minlength=bins)
-    cum, bb = 0, bins - 1
-    while bb > 0 and cum + hist[bb] < N:
-        cum += hist[bb]
-        bb -= 1
-    if cum + hist[bb] > cap:
-        return None
-    sel = np.flatnonzero(live & (b >= bb))
-    order = sorted(((s[i], int(mids[i])) for i in sel), reverse=True)
-    return [m for _, m in order[:N]]
-
-
-@pytest.mark.parametrize("seed", [0, 1, 2])
-def test_truncated_key_select_is_exact(seed):
-    """The top-N kernel keeps only 32 bits of each score key and re-scores
-    the candidates at or above the boundary bin exactly: the result equals a
-    full sort by (score, movie id) descending -- including scores that differ
-    only below the kept bits, exact ties and exclusions."""
-    rng = np.random.default_rng(seed)
-    n, N = 48859, 400
-    base = rng.normal(3.5, 0.6, n)
-    near = base[: n // 4] + rng.integers(-3, 4, n // 4) * np.finfo(np.float64).eps * 4
-    s = np.concatenate([near, base[n // 4:]])
-    s[rng.integers(0, n, 500)] = s[7]                          # exact ties
-    mids = rng.permutation(n).astype(np.int64) + 1
-    excl = np.zeros(n, bool)
-    excl[rng.integers(0, n, 300)] = True
-    got = _truncated_select(s, mids, excl, N)
-    assert got is not None
-    keep = ~excl
-    ref = sorted(zip(s[keep].tolist(), mids[keep].tolist()), reverse=True)[:N]
-    assert got == [m for _, m in ref]
