@@ -319,8 +319,9 @@ def main():
     ap.add_argument("--device-map", default=None,
                     help="test only: comma-separated GPU index per local rank "
                          "(e.g. 0,0 puts two ranks on GPU 0; needs --comm gloo)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r04.json"),
-                    help="per-kernel HBM bytes from a rocprofv3 --pmc run (optional)")
+    ap.add_argument("--pmc", default=None,
+                    help="per-kernel HBM bytes from a rocprofv3 --pmc run (optional; default "
+                         "profiles/pmc_r04.json at k = 64, profiles/pmc_r04_k<k>.json otherwise)")
     args = ap.parse_args()
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -570,8 +571,10 @@ def main():
         gather = {"bytes_per_launch": int(gb), "achieved_GBps": round(gb / avg_s / 1e9, 1),
                   "peak_GBps": GATHER_PEAK_GBS, "frac": round(gb / avg_s / 1e9 / GATHER_PEAK_GBS, 3)}
     traffic = None
-    if os.path.exists(args.pmc):
-        with open(args.pmc) as f:
+    pmc_path = args.pmc or os.path.join(
+        ROOT, "profiles", "pmc_r04.json" if k == 64 else f"pmc_r04_k{k}.json")
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
             pmc = json.load(f)
         # only for the workload the counter passes ran (per-launch bytes)
         wl = pmc.get("workload", {"shape": "ml-full", "k": 64})
