@@ -16,8 +16,11 @@ Fixtures
                                  cpp/ls/main.cpp test_als shapes), 80 % kept
   G3  als_mlshape_k<k>_it<n>.npz MovieLens-shaped sparse ids (min degree 40 /
                                  64), max_iteration = 2, 4
-  G4  band_ml100k_k10.json       held-out / train RMSE band of the reference
-                                 over seeds {0..4} x thread counts {1,2,8}
+  G4  (superseded by G12)        5-seed held-out / train RMSE band
+  G12 dist_ml100k_k{10,32}.json  the reference's distribution over 32 seeds x
+                                 thread counts {1,2,3,4,6,8} (+ the oracle's
+                                 block restatement per seed), for the
+                                 two-sample realistic-data test
   G5  als_edge_*.npz, cg_edge_sparse.npz   max_iteration 0..4, zero ratings,
                                  duplicate pairs, empty CSR rows / columns
 """
@@ -490,8 +493,7 @@ def g11():
                 train_rmse_min=float(trn.min()), train_rmse_max=float(trn.max()),
                 train_rmse_mean=float(trn.mean()), train_rmse_std=float(trn.std()),
                 meta=_meta(None))
-    with open(os.path.join(HERE, "band_ml100k_k10.json"), "w") as f:
-        json.dump(band, f, indent=1)
+    # (superseded in round 5 by g12's 32-seed dist_ml100k_k10.json; not written)
     print("G11 band test rmse", tr.min(), tr.max(), "train", trn.min(), trn.max())
     k = 32
     rs_ = synth.movielens_like("ml-100k", k, seed=synth.DATA_SEED)
@@ -517,6 +519,53 @@ def g11():
                             meta=json.dumps(_meta(1)))
         print("G11", name, "N", rs_.n, rs_.num_users, rs_.num_items, "ret", ret,
               "rets", rets, "tc spread", spread)
+    ref.set_thread_count(1)
+
+
+def _quality(U, V, k, rs_):
+    agr, n_agr = als_oracle.rank_agreement_mean(
+        U, V, k, rs_.test_user_ids, rs_.test_item_ids, rs_.test_ratings, rs_.medians)
+    return dict(train_rmse=als_oracle.rmse(U, V, rs_.user_ids, rs_.item_ids, rs_.ratings, k),
+                test_rmse=als_oracle.rmse(U, V, rs_.test_user_ids, rs_.test_item_ids,
+                                          rs_.test_ratings, k),
+                rank_agreement=agr, n_agreement_users=n_agr)
+
+
+def g12(n_seeds=32):
+    """Round 5: the realistic-data distributions for a two-sample test
+    (VERDICT r04 "do this" 1).  For C1 (ML-100K generator, k = 10) and C2
+    (the same generator shrunk at k = 32), both with 20 % of the ratings held
+    out: initial-factor seeds 0 .. n_seeds-1, the compiled reference at
+    thread counts {1, 2, 3, 4, 6, 8} per seed (``ref``: ret, train / held-out
+    RMSE, the reference's rank agreement ``my_util.py:101-145``), and the
+    oracle's block-Gram restatement of the same seed in fp64 and in the GPU
+    precision emulation (``block64`` / ``block32``), so the test can place
+    the GPU's per-seed sample against both."""
+    tcs = (1, 2, 3, 4, 6, 8)
+    for k in (10, 32):
+        rs_ = synth.movielens_like("ml-100k", k, seed=synth.DATA_SEED, test_ratio=0.2)
+        runs = []
+        for seed in range(n_seeds):
+            U0, V0 = ref.init_factors(rs_.num_users, rs_.num_items, k, seed)
+            for tc in tcs:
+                ref.set_thread_count(tc)
+                U, V, ret = ref.als(rs_.user_ids, rs_.item_ids, rs_.ratings, k, U0, V0)
+                runs.append(dict(kind="ref", seed=seed, tc=tc, ret=ret, **_quality(U, V, k, rs_)))
+            for kind, dt in (("block64", np.float64), ("block32", np.float32)):
+                U, V, ret, _ = als_oracle.als_block(rs_.user_ids, rs_.item_ids, rs_.ratings, k,
+                                                    U0, V0, dtype=dt)
+                runs.append(dict(kind=kind, seed=seed, ret=ret, **_quality(U, V, k, rs_)))
+            print("G12 k", k, "seed", seed, [(r["kind"], r.get("tc"), r["ret"],
+                                              round(r["test_rmse"], 4))
+                                             for r in runs if r["seed"] == seed], flush=True)
+        dist = dict(shape="ml-100k", k=k, data_seed=synth.DATA_SEED, test_ratio=0.2,
+                    n_train=int(rs_.n), n_test=int(len(rs_.test_ratings)),
+                    num_users=rs_.num_users, num_items=rs_.num_items,
+                    ratings_checksum=float(np.sum(rs_.ratings)),
+                    medians_checksum=float(np.sum(rs_.medians)),
+                    thread_counts=list(tcs), n_seeds=n_seeds, runs=runs, meta=_meta(None))
+        with open(os.path.join(HERE, f"dist_ml100k_k{k}.json"), "w") as f:
+            json.dump(dist, f, indent=0)
     ref.set_thread_count(1)
 
 

@@ -101,15 +101,52 @@ def test_reference_statistical_check_on_golden():
     assert np.mean(np.abs(p - d["test_ratings"])) < 0.15
 
 
-def test_band_fixture_regenerates():
-    """The G4 band's data set is regenerated bit-identically by synth."""
+@pytest.mark.parametrize("k", [10, 32])
+def test_dist_fixture_regenerates(k):
+    """The g12 distribution fixtures' data sets are regenerated bit-identically
+    by synth (the GPU test rebuilds them on the box)."""
+    import dist_stats as DS
     from movie_recommender_amd import synth
-    with open(os.path.join(GOLDEN, "band_ml100k_k10.json")) as f:
-        band = json.load(f)
-    rs = synth.movielens_like(band["shape"], band["k"], seed=band["data_seed"],
-                              test_ratio=band["test_ratio"])
-    assert rs.n == band["n_train"] and len(rs.test_ratings) == band["n_test"]
-    assert abs(float(np.sum(rs.ratings)) - band["ratings_checksum"]) < 1e-6
+    d = DS.load_dist(GOLDEN, k)
+    rs = synth.movielens_like(d["shape"], d["k"], seed=d["data_seed"], test_ratio=d["test_ratio"])
+    assert rs.n == d["n_train"] and len(rs.test_ratings) == d["n_test"]
+    assert abs(float(np.sum(rs.ratings)) - d["ratings_checksum"]) < 1e-6
+    assert abs(float(np.sum(rs.medians)) - d["medians_checksum"]) < 1e-6
+    assert len(DS.runs_of(d, "ref")) == 6 * d["n_seeds"] and d["n_seeds"] >= 20
+
+
+@pytest.mark.parametrize("k", [10, 32])
+@pytest.mark.parametrize("kind", ["block64", "block32"])
+def test_restatement_distribution_matches_reference(k, kind):
+    """The oracle's block-Gram restatement, in fp64 and in the GPU precision
+    emulation, run at the same 32 seeds (stored by g12), is a sample of the
+    reference's distribution over seeds x thread counts: two-sided
+    Mann-Whitney p >= 0.05 on held-out / train RMSE, ret, rank agreement."""
+    import dist_stats as DS
+    d = DS.load_dist(GOLDEN, k)
+    res = DS.compare(DS.runs_of(d, kind), DS.runs_of(d, "ref"))
+    assert not DS.failing(res), DS.describe(res)
+
+
+def test_dist_reference_runs_reproduce():
+    """One stored reference run of the k = 10 pool is reproduced by the
+    compiled reference (seed 3, thread counts 1 and 4)."""
+    from oracle import ref
+    if not ref.available():
+        pytest.skip("oracle/_ref not built")
+    import dist_stats as DS
+    from movie_recommender_amd import synth
+    d = DS.load_dist(GOLDEN, 10)
+    rs = synth.movielens_like(d["shape"], 10, seed=d["data_seed"], test_ratio=d["test_ratio"])
+    U0, V0 = ref.init_factors(rs.num_users, rs.num_items, 10, 3)
+    for tc in (1, 4):
+        want = [r for r in DS.runs_of(d, "ref") if r["seed"] == 3 and r["tc"] == tc][0]
+        ref.set_thread_count(tc)
+        U, V, ret = ref.als(rs.user_ids, rs.item_ids, rs.ratings, 10, U0, V0)
+        assert ret == want["ret"]
+        assert O.rmse(U, V, rs.test_user_ids, rs.test_item_ids, rs.test_ratings, 10) == \
+            pytest.approx(want["test_rmse"], rel=1e-12)
+    ref.set_thread_count(1)
 
 
 def test_exact_solve_matches_numpy_lstsq():
