@@ -71,9 +71,13 @@ typedef struct mr_stats {
  *                                     in-place all-gather of a row table:
  *                                     rank r owns rows [row_begin[r],
  *                                     row_begin[r+1]) of width row_floats
- *                                     (the engine passes its padded
- *                                     exchange buffer: equal blocks of
- *                                     maxrows rows, row_begin[r] = r maxrows)
+ *                                     (the engine passes its packed
+ *                                     exchange buffer: ONE "row" per rank,
+ *                                     row_floats = ag_block_floats(maxrows,
+ *                                     ldk, with_bias) floats wide -- the
+ *                                     rank's padded factor rows followed by
+ *                                     its biases padded to 4 -- and
+ *                                     row_begin[r] = r)
  * Both return 0 on success. */
 typedef struct mr_comm {
   void* user;

@@ -36,6 +36,9 @@ typedef struct mr_cg_stats {
   long long kernel_launches[MR_CG_K_COUNT];  /* launches that did work           */
   long long rows, cols, nnz;
   long long blocks_a, blocks_at;  /* CSR-stream row blocks of A and of A^T        */
+  long long block_max_nnz;        /* a row block's non-zero limit (longer rows:   */
+                                  /* a block of their own)                        */
+  long long block_max_rows;       /* a row block's row limit                      */
 } mr_cg_stats;
 
 /* A in the reference's CSR form: row_indices[rows+1] (int32, starting at 0,

@@ -66,7 +66,8 @@ class MrCgStats(ctypes.Structure):
                 ("kernel_launches", ctypes.c_longlong * len(CG_K_NAMES)),
                 ("rows", ctypes.c_longlong), ("cols", ctypes.c_longlong),
                 ("nnz", ctypes.c_longlong),
-                ("blocks_a", ctypes.c_longlong), ("blocks_at", ctypes.c_longlong)]
+                ("blocks_a", ctypes.c_longlong), ("blocks_at", ctypes.c_longlong),
+                ("block_max_nnz", ctypes.c_longlong), ("block_max_rows", ctypes.c_longlong)]
 
     def as_dict(self):
         return {"last_iterations": self.last_iterations,
@@ -74,7 +75,8 @@ class MrCgStats(ctypes.Structure):
                 "kernel_ms": {n: self.kernel_ms[i] for i, n in enumerate(CG_K_NAMES)},
                 "kernel_launches": {n: self.kernel_launches[i] for i, n in enumerate(CG_K_NAMES)},
                 "rows": self.rows, "cols": self.cols, "nnz": self.nnz,
-                "blocks_a": self.blocks_a, "blocks_at": self.blocks_at}
+                "blocks_a": self.blocks_a, "blocks_at": self.blocks_at,
+                "block_max_nnz": self.block_max_nnz, "block_max_rows": self.block_max_rows}
 
 
 class MrComm(ctypes.Structure):

@@ -200,6 +200,8 @@ struct CgLs {
     stats.nnz = nnz;
     stats.blocks_a = n_blk_a;
     stats.blocks_at = n_blk_t;
+    stats.block_max_nnz = kSpTile;
+    stats.block_max_rows = kSpMaxRows;
     return 0;
   }
 
@@ -376,6 +378,8 @@ int mr_cg_reset_stats(mr_cg* ctx) {
   ctx->c.stats.nnz = keep.nnz;
   ctx->c.stats.blocks_a = keep.blocks_a;
   ctx->c.stats.blocks_at = keep.blocks_at;
+  ctx->c.stats.block_max_nnz = keep.block_max_nnz;
+  ctx->c.stats.block_max_rows = keep.block_max_rows;
   return 0;
 }
 

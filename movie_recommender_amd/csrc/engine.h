@@ -29,7 +29,8 @@ struct Side {
   double *r = nullptr, *p = nullptr, *q = nullptr;     // fp64 CG vectors [E][ldk]
   double *rb = nullptr, *pb = nullptr, *qb = nullptr;  // user side: bias entries [E]
   int n_part_mv = 1;
-  int n_part_op = 1;   // one-pass CG kernel grid (resident blocks)
+  int n_part_op[2] = {1, 1};   // one-pass CG kernel grid (resident blocks) per tile
+                               // cache policy: [0] plain loads, [1] non-temporal
   double* start_parts = nullptr;   // fused CG start: (r.r, p.Gp) per block
   int64_t n_start_pairs = 0;
 };

@@ -344,15 +344,20 @@ int Engine::build_side(Side& S, bool user, int64_t n, const int32_t* d_key,
     const char* e = getenv("MR_MV_PARTS");
     return e ? (int64_t)atoll(e) : (int64_t)0;
   }();
-  int64_t op = g;
-  if (k <= kMaxK) {
-    int cus = 0;
-    MR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-    const int bpc = onepass_blocks_per_cu(S.user, k);
-    if (bpc > 0 && cus > 0) op = std::min<int64_t>(op, (int64_t)bpc * cus);
+  // (per instantiation: the plain-load and the non-temporal variant are
+  // separate code objects whose occupancy may differ; tile_nt_for picks one
+  // at launch time)
+  for (int nt = 0; nt < 2; ++nt) {
+    int64_t op = g;
+    if (k <= kMaxK) {
+      int cus = 0;
+      MR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+      const int bpc = onepass_blocks_per_cu(S.user, k, nt != 0);
+      if (bpc > 0 && cus > 0) op = std::min<int64_t>(op, (int64_t)bpc * cus);
+    }
+    if (parts_env > 0) op = std::min(g, parts_env);
+    S.n_part_op[nt] = (int)std::max<int64_t>(1, std::min<int64_t>(op, kMaxParts));
   }
-  if (parts_env > 0) op = std::min(g, parts_env);
-  S.n_part_op = (int)std::max<int64_t>(1, std::min<int64_t>(op, kMaxParts));
   MR_HIP(hipStreamSynchronize(stream));
   return 0;
 }
@@ -768,7 +773,7 @@ int Engine::allgather_side(bool user) {
     MR_D2H(tab + (size_t)rank * A.per, A.send, A.per * 4, stream);
     std::vector<long long> prb(world + 1);
     for (int r = 0; r <= world; ++r) prb[r] = r;
-    MR_CHECK(comm.allgather_rows(comm.user, tab, (int)A.per, prb.data(), world) == 0,
+    MR_CHECK(comm.allgather_rows(comm.user, tab, (long long)A.per, prb.data(), world) == 0,
              "allgather callback failed");
     MR_H2D(A.recv, tab, (size_t)world * A.per * 4, stream);
   }
@@ -1153,8 +1158,8 @@ int Engine::cg_onepass(Side& S, double min_dec, int max_it, double* final_rr, bo
     // backwards over the entities the Gram just wrote, then alternate
     const int rev = sweep == 0 ? 0 : ((t & 1) ^ (sweep == 2 ? 1 : 0));
     if (launch_cg_onepass(stream, user, d_state, t > 0 ? 1 : 0, rev, S.E, k, S.G, S.Gs, S.Gn, S.p,
-                          S.pb, S.r, S.rb, S.q, S.qb, xf, xb, xbins, S.n_part_op, d_mirror,
-                          seq_of.back(), tile_nt_for(S)))
+                          S.pb, S.r, S.rb, S.q, S.qb, xf, xb, xbins, S.n_part_op[tile_nt_for(S) ? 1 : 0],
+                          d_mirror, seq_of.back(), tile_nt_for(S)))
       return -1;
     return toc(mv_cls, t, ev);
   };

@@ -2666,12 +2666,14 @@ int op_prof_read(int64_t* out, int n) {
   return MR_OP_PROF ? n : 0;
 }
 
-int onepass_blocks_per_cu(bool user_side, int k) {
+int onepass_blocks_per_cu(bool user_side, int k, bool nt) {
   const void* f = nullptr;
 #define MR_OP_FN(NB)                                                                        \
   case NB:                                                                                  \
-    f = user_side ? (const void*)cg_onepass_kernel<NB, true, true>                          \
-                  : (const void*)cg_onepass_kernel<NB, false, true>;                        \
+    if (nt) f = user_side ? (const void*)cg_onepass_kernel<NB, true, true>                  \
+                          : (const void*)cg_onepass_kernel<NB, false, true>;                \
+    else f = user_side ? (const void*)cg_onepass_kernel<NB, true, false>                    \
+                       : (const void*)cg_onepass_kernel<NB, false, false>;                  \
     break;
   switch (nb16_of(k)) {
     MR_OP_FN(1) MR_OP_FN(2) MR_OP_FN(3) MR_OP_FN(4)

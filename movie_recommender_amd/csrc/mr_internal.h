@@ -299,7 +299,7 @@ int launch_cg_matvec(hipStream_t s, bool user_side, const CgState* st,
 // block, alpha, r'.r', the BETA rule and the publish under `seq`.  k <= 128.
 // Blocks of cg_onepass_kernel one CU holds at once for this side and k (0:
 // unknown); the one-pass grid is that times the CU count.
-int onepass_blocks_per_cu(bool user_side, int k);
+int onepass_blocks_per_cu(bool user_side, int k, bool nt);
 // diagnostic timeline of the last one-pass launch (MR_OP_PROF builds; 0 otherwise)
 int op_prof_read(int64_t* out, int n);
 int launch_cg_onepass(hipStream_t s, bool user_side, CgState* st, int update, int rev, int64_t E, int k,

@@ -33,7 +33,7 @@ def _div(a, b):
 # CG on the normal equations  (matrix.cpp:456-529, cg_least_squares)
 # --------------------------------------------------------------------------
 def cg_normal(matvec, c, x, min_r_decrease=0.01, max_iteration=200,
-              dot=None, vdtype=np.float64):
+              dot=None, vdtype=np.float64, trace=None):
     """CG on ``M x = c`` with ``M = A^T A`` given as ``matvec``.
 
     Restates ``cg_least_squares`` (``matrix.cpp:456-529``) line by line:
@@ -41,7 +41,8 @@ def cg_normal(matvec, c, x, min_r_decrease=0.01, max_iteration=200,
     rr < 1e-6 at the loop top (``:490``), two consecutive beta > 1-min_r_decrease
     failures end the solve *after* x and r were updated (``:512-518``),
     ``final_rr`` tracks the last rr computed (``:486, :508``).
-    ``x`` is updated in place.  Returns ``(iterations, final_rr)``.
+    ``x`` is updated in place.  Returns ``(iterations, final_rr)``; a list
+    passed as ``trace`` receives r0.r0 and every iteration's r'.r'.
     """
     if dot is None:
         def dot(a, b):
@@ -52,6 +53,8 @@ def cg_normal(matvec, c, x, min_r_decrease=0.01, max_iteration=200,
     fails = 0
     rr = dot(r, r)
     final_rr = rr
+    if trace is not None:
+        trace.append(rr)
     while it < max_iteration:
         if rr < 1e-6:
             return it, final_rr
@@ -61,6 +64,8 @@ def cg_normal(matvec, c, x, min_r_decrease=0.01, max_iteration=200,
         r += vdtype(alpha) * Ap if vdtype is np.float32 else alpha * Ap
         rr2 = dot(r, r)
         final_rr = rr2
+        if trace is not None:
+            trace.append(rr2)
         beta = _div(rr2, rr)
         if beta > 1 - min_r_decrease:
             fails += 1
@@ -235,12 +240,12 @@ def block_matvec(G):
     return mv
 
 
-def cg_blocks(G, c, x, min_r_decrease=0.01, max_iteration=200):
+def cg_blocks(G, c, x, min_r_decrease=0.01, max_iteration=200, trace=None):
     """Block-Gram CG: ``cg_normal`` with the batched block GEMV.  Vectors are
     fp64; ``x`` keeps its own dtype (fp32 factor tables: x += alpha p is
     formed in fp64 and rounded)."""
     return cg_normal(block_matvec(G), np.asarray(c, np.float64).reshape(-1), x,
-                     min_r_decrease, max_iteration)
+                     min_r_decrease, max_iteration, trace=trace)
 
 
 def als_block(user_ids, item_ids, ratings, k, U0, V0,

@@ -179,11 +179,13 @@ def peer_missing_rank(d, rank, world, out):
 
 
 def comm_padded(rank, world):
-    """The callback transport's host side as the engine drives it: the padded
-    exchange table (world x maxrows rows, this rank's packed block at
-    rank x maxrows) through TorchComm's allgather_rows with padded row
-    boundaries, then the bias column (1 float per row); returns the gathered
-    tables for rank 0 to compare with the expected blocks."""
+    """The callback transport's host side on generic row tables: a table of
+    world x maxrows rows of ldk floats (this rank's rows at rank x maxrows)
+    and a 1-float-per-row column, through TorchComm's allgather_rows with
+    row boundaries r x maxrows; returns the gathered tables for rank 0 to
+    compare with the expected blocks.  (The engine itself passes ONE row per
+    rank, ag_block_floats(maxrows, ldk, with_bias) floats wide, row_begin[r]
+    = r -- the world 2 / 3 engine tests drive that layout.)"""
     import ctypes
     from movie_recommender_amd.distributed import TorchComm
     comm = TorchComm()

@@ -121,7 +121,11 @@ def test_cg_context_reuse_and_stats(gpu):
         for c in ("spmv_a", "spmv_at", "update"):
             assert total <= s["kernel_launches"][c] <= total + 3, (c, s["kernel_launches"])
         assert s["kernel_launches"]["setup"] == 3 and s["solve_ms"] > 0
-        assert s["blocks_a"] == -(-(len(rp) - 1) // 204)   # 10 nnz/row: 204 rows per block
+        # the row blocks restated from the limits the library reports (every
+        # row of this matrix holds 10 non-zeros, so the greedy cut gives
+        # blocks of min(max_rows, max_nnz // 10) rows whatever the row order)
+        per_block = min(s["block_max_rows"], s["block_max_nnz"] // 10)
+        assert s["block_max_nnz"] >= 10 and s["blocks_a"] == -(-(len(rp) - 1) // per_block)
     finally:
         L.mr_cg_destroy(h)
 
