@@ -331,7 +331,7 @@ int Engine::build_side(Side& S, bool user, int64_t n, const int32_t* d_key,
     MR_HIP(hipMemsetAsync(S.qb, 0, S.E * sizeof(double), stream));
   }
   // fused CG start: one (r.r, p.Gp, q.q) triple per Gram block, then per split block
-  S.n_start_pairs = gram_blocks(S.n_work) + (S.n_split + 3) / 4;
+  S.n_start_pairs = gram_blocks(S.n_work, k) + (S.n_split + 3) / 4;
   if (dalloc(&S.start_parts, 3 * std::max<int64_t>(1, S.n_start_pairs), stream)) return -1;
   // matvec grid: one wave per entity, fixed grid for reproducible partials
   const int64_t g = (S.E + 3) / 4;
@@ -956,7 +956,7 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr, bool start
       const CgStart cs = cg_start_of(S);
       if (tic(MR_K_CG_START, -1, &a)) return -1;
       if (launch_cg_start_split(stream, user, k, S.split, S.n_split, direct_dst(S), cs,
-                                S.start_parts + 3 * gram_blocks(S.n_work)))
+                                S.start_parts + 3 * gram_blocks(S.n_work, k)))
         return -1;
       if (toc(MR_K_CG_START, -1, a)) return -1;
     }
@@ -1120,7 +1120,7 @@ int Engine::cg_onepass(Side& S, double min_dec, int max_it, double* final_rr, bo
       StartFold fold{d_state, d_mirror, seq_of[0], min_dec, max_it, 2};
       if (tic(MR_K_CG_START, -1, &a)) return -1;
       if (launch_cg_start_split(stream, user, k, S.split, S.n_split, direct_dst(S), cs,
-                                S.start_parts + 3 * gram_blocks(S.n_work), fold))
+                                S.start_parts + 3 * gram_blocks(S.n_work, k), fold))
         return -1;
       if (toc(MR_K_CG_START, -1, a)) return -1;
     } else {

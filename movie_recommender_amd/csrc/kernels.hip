@@ -717,10 +717,26 @@ __host__ __device__ constexpr int acc_tile(int bi, int bj, int nb) {
 // loop's register budget (3 waves per SIMD at k = 64), so tile conversions
 // are not hoisted (sched_barrier).  v in sc.pv (virtual order).  Returns y at virtual
 // o = lane + 64 h in yo[h] (without the bias column) -- 0 for padding.
-template <int NB>
-__device__ __forceinline__ void acc_matvec(const floatx4 (&acc)[NB * (NB + 1) / 2],
-                                           StartScratch<NB>& sc, int k,
-                                           double (&yo)[(16 * NB + 63) / 64]) {
+// TILE(bi, bj) returns the accumulator tile of upper block (bi, bj) (the Gram
+// wave's own registers, or -- the NB = 8 pair kernel -- the partner wave's LDS
+// dump).
+// OWN(bi, bj): whether this wave holds block (bi, bj) (the pair kernel's
+// split start: each wave takes its own tiles' products, the two partial
+// results are added afterwards); partR / yC: where the row partials and the
+// column sums go.
+template <int NB, bool SB, class TILE, class OWN>
+__device__ __forceinline__ void acc_matvec_g(TILE&& tile, OWN&& own, StartScratch<NB>& sc,
+                                             double (*partR)[64], double* yC, int k,
+                                             double (&yo)[(16 * NB + 63) / 64]);
+template <int NB, bool SB = false, class TILE>
+__device__ __forceinline__ void acc_matvec_t(TILE&& tile, StartScratch<NB>& sc, int k,
+                                             double (&yo)[(16 * NB + 63) / 64]) {
+  acc_matvec_g<NB, SB>(tile, [](int, int) { return true; }, sc, sc.partR, sc.yC, k, yo);
+}
+template <int NB, bool SB, class TILE, class OWN>
+__device__ __forceinline__ void acc_matvec_g(TILE&& tile, OWN&& own, StartScratch<NB>& sc,
+                                             double (*partR)[64], double* yC, int k,
+                                             double (&yo)[(16 * NB + 63) / 64]) {
   constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
   const int lane = threadIdx.x & 63, q = lane >> 4, col = lane & 15;
   // One pass over the upper tiles, block rows in order, each row starting at
@@ -742,12 +758,13 @@ __device__ __forceinline__ void acc_matvec(const floatx4 (&acc)[NB * (NB + 1) / 
     const double vr[4] = {va.x, va.y, vb.x, vb.y};   // v_bi at rows 4q + r
 #pragma unroll
     for (int bj = bi; bj < NB; ++bj) {
-      const int t = acc_tile(bi, bj, NB);
+      if (!own(bi, bj)) continue;
       const double vj = sc.pv[16 * bj + col];
+      const floatx4 at = tile(bi, bj);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = 4 * q + r;
-        const double a = (double)acc[t][r];
+        const double a = (double)at[r];
         // diagonal block: the bf16x3 sum is not bitwise symmetric, so use
         // exactly the triangle tri16 stores (upper for even blocks and the
         // odd last block, lower + side diagonal for odd folded blocks); the
@@ -759,13 +776,17 @@ __device__ __forceinline__ void acc_matvec(const floatx4 (&acc)[NB * (NB + 1) / 
       }
 #ifdef MR_ACC_SB   // per-tile scheduling barrier (off: Gram users / items -1 %)
       __builtin_amdgcn_sched_barrier(0);
+#else
+      // SB (the pair kernel, whose tiles partly come from LDS): one tile's
+      // loads at a time, not all 36 hoisted
+      if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
 #endif
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) sc.partR[4 * bi + r][lane] = R[r];
+    for (int r = 0; r < 4; ++r) partR[4 * bi + r][lane] = R[r];
     double c = xor_sum_f64<16>(cc[bi]);
     c = xor_sum_f64<32>(c);   // identical in all 4 rows
-    if (q == 0) sc.yC[16 * bi + col] = c;
+    if (q == 0) yC[16 * bi + col] = c;
   }
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -775,7 +796,7 @@ __device__ __forceinline__ void acc_matvec(const floatx4 (&acc)[NB * (NB + 1) / 
     if (o >= NP || nat_of(o, NB) >= k) continue;
     // row 4q + r of block b: the 16 lanes (q, 0..15) of partial r
     const int b = o >> 4, i = o & 15;
-    const double2* pr = reinterpret_cast<const double2*>(&sc.partR[4 * b + (i & 3)][16 * (i >> 2)]);
+    const double2* pr = reinterpret_cast<const double2*>(&partR[4 * b + (i & 3)][16 * (i >> 2)]);
     double s[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -783,9 +804,15 @@ __device__ __forceinline__ void acc_matvec(const floatx4 (&acc)[NB * (NB + 1) / 
       s[j] = v.x + v.y;
     }
     const double rs = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
-    yo[h] = rs + sc.yC[o];
+    yo[h] = rs + yC[o];
   }
   __builtin_amdgcn_wave_barrier();
+}
+template <int NB>
+__device__ __forceinline__ void acc_matvec(const floatx4 (&acc)[NB * (NB + 1) / 2],
+                                           StartScratch<NB>& sc, int k,
+                                           double (&yo)[(16 * NB + 63) / 64]) {
+  acc_matvec_t<NB>([&](int bi, int bj) { return acc[acc_tile(bi, bj, NB)]; }, sc, k, yo);
 }
 
 // Fused CG start of one unsplit entity from the Gram wave's registers
@@ -795,30 +822,44 @@ __device__ __forceinline__ void acc_matvec(const floatx4 (&acc)[NB * (NB + 1) / 
 // (lane partials summed across the wave).  cacc / sacc: c and the row sums at virtual
 // (b, col) in every lane (already reduced over q); wt / gn: user-side
 // sum of ratings and count; xv / xb: x at virtual (b, col) and its bias.
-template <int NB, bool USER>
-__device__ __forceinline__ void start_from_acc(const floatx4 (&acc)[NB * (NB + 1) / 2],
-                                               const float (&cacc)[NB], const float (&sacc)[NB],
-                                               float wt, float gn, const float (&xv)[NB],
-                                               float xb, int64_t e, int k, int ldk,
-                                               const CgStart& cs, StartScratch<NB>& sc,
-                                               double& drr, double& dpq, double& dqq) {
-  constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
+// The start's inputs in StartScratch (lanes q == 0): x (virtual order) for
+// the NB segments in [b0, b1), and c / the row sums of those segments.
+template <int NB, bool USER, int NL>
+__device__ __forceinline__ void start_stage(const float (&cacc)[NL], const float (&sacc)[NL],
+                                            int b0, int k, StartScratch<NB>& sc) {
   const int lane = threadIdx.x & 63, q = lane >> 4, col = lane & 15;
   if (q == 0) {
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
+    for (int j = 0; j < NL; ++j) {
+      const int b = b0 + j;
       const bool live = NB * col + b < k;   // natural column of virtual (b, col)
-      sc.pv[16 * b + col] = xv[b];
-      sc.sC[16 * b + col] = live ? cacc[b] : 0.f;
-      if (USER) sc.sGs[16 * b + col] = live ? sacc[b] : 0.f;
+      sc.sC[16 * b + col] = live ? cacc[j] : 0.f;
+      if (USER) sc.sGs[16 * b + col] = live ? sacc[j] : 0.f;
     }
   }
-  __builtin_amdgcn_wave_barrier();
-  double yo[NV];
-  acc_matvec<NB>(acc, sc, k, yo);
-  // r0 = G x - c (+ bias column), p0 = -r0; user bias row: Gs.x + Gn xb - Cb
+}
+template <int NB>
+__device__ __forceinline__ void start_stage_x(const float (&xv)[NB], StartScratch<NB>& sc) {
+  const int lane = threadIdx.x & 63, q = lane >> 4, col = lane & 15;
+  if (q == 0) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) sc.pv[16 * b + col] = xv[b];
+  }
+}
+// The start itself once its inputs are staged (start_stage / start_stage_x),
+// on the accumulator tiles TILE(t).
+// The start after y = G x (yo, virtual order): r0 = y - c (+ bias column),
+// p0 = -r0 written to the CG vectors, r0.r0 added to drr, p0 into sc.pv
+// (and pn / pb for the q0 step).
+template <int NB, bool USER>
+__device__ __forceinline__ void start_r0(const double (&yo)[(16 * NB + 63) / 64], float wt,
+                                         float gn, float xb, int64_t e, int k, int ldk,
+                                         const CgStart& cs, StartScratch<NB>& sc, double& drr,
+                                         double (&pn)[(16 * NB + 63) / 64], double& pb) {
+  constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
+  const int lane = threadIdx.x & 63;
   const double xbd = xb;
-  double d = 0.0, ybp = 0.0, pn[NV];
+  double d = 0.0, ybp = 0.0;
 #pragma unroll
   for (int h = 0; h < NV; ++h) {
     const int o = lane + 64 * h;
@@ -840,7 +881,7 @@ __device__ __forceinline__ void start_from_acc(const floatx4 (&acc)[NB * (NB + 1
       }
     }
   }
-  double pb = 0.0;
+  pb = 0.0;
   if (USER) {
     const double rbv = fma((double)gn, xbd, wave_sum_f64(ybp)) - (double)wt;
     pb = -rbv;
@@ -858,11 +899,16 @@ __device__ __forceinline__ void start_from_acc(const floatx4 (&acc)[NB * (NB + 1
     if (o < NP) sc.pv[o] = pn[h];
   }
   __builtin_amdgcn_wave_barrier();
-  // q0 = G p0 (+ bias column), p0.q0
-  acc_matvec<NB>(acc, sc, k, yo);
-  d = 0.0;
-  ybp = 0.0;
-  double dq = 0.0;
+}
+// The start after q0 = G p0 (yo): q0 written, p0.q0 and q0.q0 added.
+template <int NB, bool USER>
+__device__ __forceinline__ void start_q0(const double (&yo)[(16 * NB + 63) / 64], float gn,
+                                         double pb, const double (&pn)[(16 * NB + 63) / 64],
+                                         int64_t e, int k, int ldk, const CgStart& cs,
+                                         StartScratch<NB>& sc, double& dpq, double& dqq) {
+  constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
+  const int lane = threadIdx.x & 63;
+  double d = 0.0, ybp = 0.0, dq = 0.0;
 #pragma unroll
   for (int h = 0; h < NV; ++h) {
     const int o = lane + 64 * h;
@@ -891,6 +937,34 @@ __device__ __forceinline__ void start_from_acc(const floatx4 (&acc)[NB * (NB + 1
   }
   dpq += wave_sum_f64(d);
   dqq += wave_sum_f64(dq);
+}
+// The start itself once its inputs are staged (start_stage / start_stage_x),
+// on the accumulator tiles TILE(bi, bj).
+template <int NB, bool USER, bool SB = false, class TILE>
+__device__ __forceinline__ void start_from_tiles(TILE&& tile, float wt, float gn, float xb,
+                                                 int64_t e, int k, int ldk, const CgStart& cs,
+                                                 StartScratch<NB>& sc, double& drr, double& dpq,
+                                                 double& dqq) {
+  constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
+  __builtin_amdgcn_wave_barrier();
+  double yo[NV], pn[NV], pb;
+  acc_matvec_t<NB, SB>(tile, sc, k, yo);
+  start_r0<NB, USER>(yo, wt, gn, xb, e, k, ldk, cs, sc, drr, pn, pb);
+  // q0 = G p0 (+ bias column), p0.q0
+  acc_matvec_t<NB, SB>(tile, sc, k, yo);
+  start_q0<NB, USER>(yo, gn, pb, pn, e, k, ldk, cs, sc, dpq, dqq);
+}
+template <int NB, bool USER>
+__device__ __forceinline__ void start_from_acc(const floatx4 (&acc)[NB * (NB + 1) / 2],
+                                               const float (&cacc)[NB], const float (&sacc)[NB],
+                                               float wt, float gn, const float (&xv)[NB],
+                                               float xb, int64_t e, int k, int ldk,
+                                               const CgStart& cs, StartScratch<NB>& sc,
+                                               double& drr, double& dpq, double& dqq) {
+  start_stage_x<NB>(xv, sc);
+  start_stage<NB, USER, NB>(cacc, sacc, 0, k, sc);
+  start_from_tiles<NB, USER>([&](int bi, int bj) { return acc[acc_tile(bi, bj, NB)]; }, wt, gn,
+                             xb, e, k, ldk, cs, sc, drr, dpq, dqq);
 }
 
 // ---------------------------------------------------------------------------
@@ -1383,6 +1457,482 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 3 : 1)) void gram_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// K1 at NB = 8 (k = 113 ... 128, the C4 / C5 shapes): one work item on a PAIR
+// of waves (round 5).  The one-wave form holds all 36 upper blocks (144
+// AGPRs) beside the three bf16 parts of 8 segments (96 VGPRs) and the
+// gathered rows: one wave per SIMD, issue-bound, the row-gather latency and
+// the epilogue exposed.  Here wave r ("role") of a 128-thread block owns
+// segments 4r .. 4r+3 of every gathered row (one dwordx4 per row per lane:
+// half the gather instructions), splits them, and accumulates 18 blocks:
+//   role 0: the 10 blocks inside segments 0-3, and (bi, bj), bi <= 3, bj = 4, 5
+//   role 1: the 10 blocks inside segments 4-7, and (bi, bj), bi <= 3, bj = 6, 7
+// so role 0 reads the partner's parts of segments 4, 5 and role 1 those of
+// segments 0-3 from an LDS stage written once per 32-rating half (two
+// barriers per half).  Every block is still accumulated by ONE wave, over the
+// same halves with the same six products in the same order, so G is
+// bitwise the one-wave kernel's.  Epilogue: each wave stores its own tiles
+// (role 0 holds the folded diagonal pairs 0-1 and 2-3, role 1 4-5 and 6-7);
+// the fused CG start runs on role 1 with role 0's tiles dumped into the
+// (then free) stage -- the same acc_matvec arithmetic, so the start is
+// bitwise the one-wave kernel's too.  Accumulators in VGPRs (mfma_acc), at
+// most 256 registers per wave: two waves per SIMD.
+// ---------------------------------------------------------------------------
+constexpr int PAIR_T = 18;   // upper blocks per wave
+// MR_PAIR_PREFETCH: the next half's rows are gathered while this half's
+// MFMAs run (1, default) or after them (0).  MR_PAIR_SPLIT_START: the fused
+// CG start split over both waves (1, default) or run by role 1 on a dump of
+// role 0's tiles (0, bitwise the one-wave kernel's start).  Same box, fixed
+// 10 CG iterations, ML-full k = 128 users / items Gram (profiles/r05/ab_pair):
+// one wave 1.230 / 0.957 ms; pair 1.069-1.084 / 0.849-0.868 (both 0);
+// prefetch 1.088 / 0.851; split start 1.084 / 0.868; both 1.058 / 0.838 ms.
+#ifndef MR_PAIR_PREFETCH
+#define MR_PAIR_PREFETCH 1
+#endif
+#ifndef MR_PAIR_SPLIT_START
+#define MR_PAIR_SPLIT_START 1
+#endif
+__host__ __device__ constexpr int pair_owner(int bi, int bj) { return (bi <= 3 && bj <= 5) ? 0 : 1; }
+__host__ __device__ constexpr int pair_local(int bi, int bj) {
+  return pair_owner(bi, bj) == 0 ? (bj <= 3 ? acc_tile(bi, bj, 4) : 10 + 4 * (bj - 4) + bi)
+                                 : (bi >= 4 ? acc_tile(bi - 4, bj - 4, 4) : 10 + 2 * bi + (bj - 6));
+}
+constexpr bool pair_partition_ok() {
+  int seen[2][PAIR_T] = {};
+  for (int bi = 0; bi < 8; ++bi)
+    for (int bj = bi; bj < 8; ++bj) {
+      const int o = pair_owner(bi, bj), l = pair_local(bi, bj);
+      if (l < 0 || l >= PAIR_T || seen[o][l]) return false;
+      seen[o][l] = 1;
+    }
+  return true;
+}
+static_assert(pair_partition_ok(), "the two waves' block lists must partition the 36 blocks");
+// LDS stage of the partner parts: [segment 0..5][part][lane]; the same 1,152
+// 16-byte slots hold role 0's 18 accumulator tiles in the epilogue
+constexpr int PAIR_STAGE = 6 * 3 * 64;
+static_assert(PAIR_STAGE == PAIR_T * 64, "stage and tile dump share the LDS array");
+
+// Accumulators in arch VGPRs ("+v": the VGPR form of the MFMA): a kernel
+// that uses no AGPR gets the whole 256-register budget of 2 waves / SIMD as
+// VGPRs, where any AGPR use makes the allocator split it 128 / 128.
+__device__ __forceinline__ void mfma_acc(floatx4& acc, const u32x4_t& a, const u32x4_t& b) {
+  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+}
+// mfma_exit_guard for VGPR accumulators: 20 wait states between the last
+// MFMA and any reader of its result, in a statement that takes every
+// accumulator as an operand (so no copy or read of one is scheduled above it)
+template <int T, int TW>
+__device__ __forceinline__ void mfma_exit_guard_v(floatx4 (&acc)[T], floatx4 (&accw)[TW]) {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]));
+#pragma unroll
+  for (int g = 4; g < T; g += 2) {
+    __builtin_amdgcn_sched_barrier(0);
+    if (g + 1 < T) asm volatile("" : "+v"(acc[g]), "+v"(acc[g + 1]));
+    else asm volatile("" : "+v"(acc[g]));
+  }
+#pragma unroll
+  for (int g = 0; g < TW; ++g) {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" : "+v"(accw[g]));
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+// s_waitcnt lgkmcnt(0) as the builtin (vmcnt / expcnt left at their maximum),
+// so the waitcnt pass sees the partner operands already waited for and puts
+// nothing between mfma_entry_guard's nops and the first MFMA
+__device__ __forceinline__ void lds_wait() { __builtin_amdgcn_s_waitcnt(0xC07F); }
+
+// One half's MFMAs of a role (products hh, hm, mh, hl, lh, mm per block, in
+// that order, as bf3_mfma).  P: this wave's own segments' parts; stg: the
+// stage with the partner's.
+template <int ROLE, bool USER>
+__device__ __forceinline__ void pair_mfma(floatx4 (&acc)[PAIR_T], floatx4 (&accw)[4],
+                                          const u32x4_t (&P)[3][4], const u32x4_t& W,
+                                          bool rhs_mfma, const u32x4_t* __restrict__ stg,
+                                          int lane) {
+  auto seg = [&](u32x4_t (&X)[3], int s) {
+    X[0] = stg[(3 * s + 0) * 64 + lane];
+    X[1] = stg[(3 * s + 1) * 64 + lane];
+    X[2] = stg[(3 * s + 2) * 64 + lane];
+  };
+  u32x4_t X[3], Y[3];
+  if constexpr (ROLE == 0) {
+    seg(X, 4);
+    seg(Y, 5);
+    mfma_entry_guard();
+#pragma unroll
+    for (int sidx = 0; sidx < 6; ++sidx) {
+      const int pa = (sidx == 2) ? 1 : (sidx == 4) ? 2 : (sidx == 5) ? 1 : 0;
+      const int pb = (sidx == 1) ? 1 : (sidx == 3) ? 2 : (sidx == 5) ? 1 : 0;
+#pragma unroll
+      for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+        for (int bj = bi; bj < 4; ++bj) mfma_acc(acc[acc_tile(bi, bj, 4)], P[pa][bi], P[pb][bj]);
+    }
+    lds_wait();
+    mfma_entry_guard();
+#pragma unroll
+    for (int sidx = 0; sidx < 6; ++sidx) {
+      const int pa = (sidx == 2) ? 1 : (sidx == 4) ? 2 : (sidx == 5) ? 1 : 0;
+      const int pb = (sidx == 1) ? 1 : (sidx == 3) ? 2 : (sidx == 5) ? 1 : 0;
+#pragma unroll
+      for (int bi = 0; bi < 4; ++bi) mfma_acc(acc[10 + bi], P[pa][bi], X[pb]);
+#pragma unroll
+      for (int bi = 0; bi < 4; ++bi) mfma_acc(acc[14 + bi], P[pa][bi], Y[pb]);
+    }
+  } else {
+    seg(X, 0);
+    seg(Y, 1);
+    mfma_entry_guard();
+#pragma unroll
+    for (int sidx = 0; sidx < 6; ++sidx) {
+      const int pa = (sidx == 2) ? 1 : (sidx == 4) ? 2 : (sidx == 5) ? 1 : 0;
+      const int pb = (sidx == 1) ? 1 : (sidx == 3) ? 2 : (sidx == 5) ? 1 : 0;
+#pragma unroll
+      for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+        for (int bj = bi; bj < 4; ++bj) mfma_acc(acc[acc_tile(bi, bj, 4)], P[pa][bi], P[pb][bj]);
+    }
+    lds_wait();
+    mfma_entry_guard();
+#pragma unroll
+    for (int sidx = 0; sidx < 6; ++sidx) {
+      const int pa = (sidx == 2) ? 1 : (sidx == 4) ? 2 : (sidx == 5) ? 1 : 0;
+      const int pb = (sidx == 1) ? 1 : (sidx == 3) ? 2 : (sidx == 5) ? 1 : 0;
+      mfma_acc(acc[10], X[pa], P[pb][2]);
+      mfma_acc(acc[11], X[pa], P[pb][3]);
+      mfma_acc(acc[12], Y[pa], P[pb][2]);
+      mfma_acc(acc[13], Y[pa], P[pb][3]);
+    }
+    seg(X, 2);
+    seg(Y, 3);
+    lds_wait();
+    mfma_entry_guard();
+#pragma unroll
+    for (int sidx = 0; sidx < 6; ++sidx) {
+      const int pa = (sidx == 2) ? 1 : (sidx == 4) ? 2 : (sidx == 5) ? 1 : 0;
+      const int pb = (sidx == 1) ? 1 : (sidx == 3) ? 2 : (sidx == 5) ? 1 : 0;
+      mfma_acc(acc[14], X[pa], P[pb][2]);
+      mfma_acc(acc[15], X[pa], P[pb][3]);
+      mfma_acc(acc[16], Y[pa], P[pb][2]);
+      mfma_acc(acc[17], Y[pa], P[pb][3]);
+    }
+  }
+  if (USER && rhs_mfma) {   // the W block of this wave's segments (bf3_mfma)
+#pragma unroll
+    for (int part = 0; part < 3; ++part)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) mfma_acc(accw[b], P[part][b], W);
+  }
+}
+
+// the segments a role writes into the stage for its partner (written out
+// statement by statement: as a loop nest the compiler kept P in scratch
+// memory and copied it with a runtime-indexed loop)
+template <int S0, int PS, int... I>
+__device__ __forceinline__ void pair_stage_put(const u32x4_t (&P)[3][4], u32x4_t* __restrict__ stg,
+                                               int lane, std::integer_sequence<int, I...>) {
+  ((stg[(3 * (S0 + I / 3) + I % 3) * 64 + lane] = P[I % 3][PS + I / 3]), ...);
+}
+template <int ROLE>
+__device__ __forceinline__ void pair_stage_write(const u32x4_t (&P)[3][4],
+                                                 u32x4_t* __restrict__ stg, int lane) {
+  if constexpr (ROLE == 0) pair_stage_put<0, 0>(P, stg, lane, std::make_integer_sequence<int, 12>{});
+  else pair_stage_put<4, 0>(P, stg, lane, std::make_integer_sequence<int, 6>{});
+}
+
+// Work-list position of pair block b: the list deals range x's chunks to
+// positions p with (p / 4) mod 8 == x (four waves per one-wave Gram block,
+// block b on XCD b mod 8); with one work item per block the same XCD holds
+// position p = 32 g + 4 x + j for block b = 32 g + 8 j + x (a bijection on
+// every full group of 32; the tail keeps p = b).
+__device__ __forceinline__ int64_t pair_pos(int64_t b, int64_t n) {
+  if (b >= (n & ~(int64_t)31)) return b;
+  return 32 * (b >> 5) + 4 * (b & 7) + ((b >> 3) & 3);
+}
+
+// One wave of the pair, its role a template parameter: each role's code is
+// compiled on its own (a runtime role made the compiler keep P in scratch).
+template <int ROLE, bool USER, bool FUSE, bool BUF, bool RHSM>
+__device__ __forceinline__ void gram_pair_wave(
+    const WorkItem* __restrict__ work, int64_t n_work,
+    const int32_t* __restrict__ idx, const float* __restrict__ val,
+    const float* __restrict__ F, const float* __restrict__ bias, int k, int ldk, int zrow,
+    const GramDst& direct, const GramDst& slab, const CgStart& cs, u32x4_t* __restrict__ stg,
+    StartScratch<8>& sc) {
+  constexpr int NB = 8;
+  constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2, NTILE = NO + NF;
+  constexpr int role = ROLE;
+  const int lane = threadIdx.x & 63;
+  const int64_t wi = pair_pos(blockIdx.x, n_work);
+  const bool rhs_mfma = USER && RHSM;
+  double drr = 0.0, dpq = 0.0, dqq = 0.0;
+  const int64_t wbeg = work[wi].begin;
+  const int wlen = work[wi].len;
+  const int went = work[wi].entity;
+  const int wslab = work[wi].slab;
+  const int q = lane >> 4, col = lane & 15;
+  const int64_t end = wbeg + wlen;
+  constexpr uint32_t row_bytes = 64u * NB;
+  // this wave's 4 segments: floats 4 role .. 4 role + 3 of the lane's 8
+  RowSrc src;
+  src.Fc = reinterpret_cast<const char*>(F) + 4 * NB * col + 16 * role;
+  src.colb = 4u * NB * (uint32_t)col + 16u * (uint32_t)role;
+  if constexpr (BUF)
+    src.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(F), (short)0,
+                                                 (int)((uint32_t)(zrow + 1) * row_bytes),
+                                                 0x00020000);
+  floatx4 acc[PAIR_T];
+#pragma unroll
+  for (int t = 0; t < PAIR_T; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  floatx4 accw[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) accw[b] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float cacc[4], sacc[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) { cacc[b] = 0.f; sacc[b] = 0.f; }
+  float wsum = 0.f;
+  const int64_t safe = wlen > 0 ? wbeg : 0;
+  const int slot = half_slot(lane);
+  auto ld32 = [&](int c) {
+    const int64_t jj = wbeg + 32 * (int64_t)c + slot;
+    ChunkRaw r;
+    const int64_t js = jj < end ? jj : safe;
+    r.idx = idx[js];
+    r.r = val[js];
+    r.b = 0.f;
+    return r;
+  };
+  auto bias32 = [&](ChunkRaw& cr, int c) {
+    if (!USER) {
+      const bool ok = wbeg + 32 * (int64_t)c + slot < end;
+      cr.b = bias[ok ? cr.idx : zrow];
+    }
+  };
+  auto fin32 = [&](const ChunkRaw& cr, int c) {
+    const bool ok = wbeg + 32 * (int64_t)c + slot < end;
+    ChunkRegs r;
+    r.idx = ok ? cr.idx : zrow;
+    r.w = ok ? cr.r - cr.b : 0.f;
+    return r;
+  };
+  ChunkRaw h1 = ld32(1), h2 = ld32(2);
+  ChunkRaw h0 = ld32(0);
+  bias32(h0, 0);
+  bias32(h1, 1);
+  float Fr[8][4], w[8];
+  u32x4_t P[3][4], W;
+  gather_half<4, BUF>(Fr, w, fin32(h0, 0), src, row_bytes);
+  bf3_split<4, USER>(P, W, cacc, sacc, wsum, Fr, w, rhs_mfma);
+  pair_stage_write<ROLE>(P, stg, lane);
+  __syncthreads();
+  const int nhalves = (wlen + 31) >> 5;
+  for (int h = 0; h < nhalves - 1; ++h) {
+    const ChunkRaw h3 = ld32(h + 3);
+    bias32(h2, h + 2);
+#if MR_PAIR_PREFETCH
+    // the next half's rows in flight during this half's MFMAs
+    gather_half<4, BUF>(Fr, w, fin32(h1, h + 1), src, row_bytes);
+    pair_mfma<ROLE, USER>(acc, accw, P, W, rhs_mfma, stg, lane);
+#else
+    // the next half's rows gathered after this half's MFMAs are issued (a
+    // second wave per SIMD, of another pair, covers the latency)
+    pair_mfma<ROLE, USER>(acc, accw, P, W, rhs_mfma, stg, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    gather_half<4, BUF>(Fr, w, fin32(h1, h + 1), src, row_bytes);
+#endif
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();   // both waves done reading this half's stage
+    bf3_split<4, USER>(P, W, cacc, sacc, wsum, Fr, w, rhs_mfma);
+    pair_stage_write<ROLE>(P, stg, lane);
+    __syncthreads();   // the next half's stage complete
+    h1 = h2;
+    h2 = h3;
+  }
+  if (nhalves > 0) pair_mfma<ROLE, USER>(acc, accw, P, W, rhs_mfma, stg, lane);
+  mfma_exit_guard_v(acc, accw);
+
+  // ---- epilogue (gram_wave's, over this wave's segments and blocks) -------
+  if (rhs_mfma) {
+    const int s0 = 16 * (col >> 2), r = col & 3;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      float v0[4], v1[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v0[j] = __shfl(accw[b][j], s0, 64);
+        v1[j] = __shfl(accw[b][j], s0 + 1, 64);
+      }
+      sacc[b] = r == 0 ? v1[0] : r == 1 ? v1[1] : r == 2 ? v1[2] : v1[3];
+      cacc[b] = r == 0 ? v0[0] : r == 1 ? v0[1] : r == 2 ? v0[2] : v0[3];
+    }
+  } else {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      cacc[b] = xor_sum_f32<16>(cacc[b]);
+      cacc[b] = xor_sum_f32<32>(cacc[b]);
+      if (USER) {
+        sacc[b] = xor_sum_f32<16>(sacc[b]);
+        sacc[b] = xor_sum_f32<32>(sacc[b]);
+      }
+    }
+  }
+  const bool to_slab = wslab >= 0;
+  const int64_t di = to_slab ? (int64_t)wslab : (int64_t)went;
+  const GramDst& D = to_slab ? slab : direct;
+  float* __restrict__ Gd = D.G + di * D.sG;
+  float* __restrict__ Cd = D.C + di * D.sV;
+  if (q == 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = NB * col + 4 * role + j;   // natural column of virtual (4 role + j, col)
+      Cd[c] = (c < k) ? cacc[j] : 0.f;
+      if (USER) D.Gs[di * D.sV + c] = (c < k) ? sacc[j] : 0.f;
+    }
+  }
+  auto lane_f32 = [](float v, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+  };
+  const float wt = USER ? (lane_f32(wsum, 0) + lane_f32(wsum, 16)) +
+                              (lane_f32(wsum, 32) + lane_f32(wsum, 48))
+                        : 0.f;
+  if (USER && role == 0 && lane == 0) {
+    D.Cb[di * D.sS] = wt;
+    D.Gn[di * D.sS] = (float)wlen;
+  }
+  float* __restrict__ Gl = Gd + 64 * q + col;
+  auto store_tiles = [&](auto own) {
+#pragma unroll
+    for (int bi = 0; bi < NB; ++bi) {
+#pragma unroll
+      for (int bj = bi + 1; bj < NB; ++bj) {
+        if (pair_owner(bi, bj) != decltype(own)::value) continue;
+        const int t = pair_local(bi, bj), o = off_index(bi, bj, NB) * 256;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Gl[o + 16 * r] = acc[t][r];
+      }
+    }
+#pragma unroll
+    for (int m = 2 * decltype(own)::value; m < 2 * decltype(own)::value + 2; ++m) {
+      const int te = pair_local(2 * m, 2 * m), to = pair_local(2 * m + 1, 2 * m + 1);
+      float dg = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 4 * q + r;
+        Gl[(NO + m) * 256 + 16 * r] = col >= row ? acc[te][r] : acc[to][r];
+        if (col - 4 * q == r) dg = acc[to][r];
+      }
+      if ((col >> 2) == q) Gd[NTILE * 256 + m * 16 + col] = dg;   // D_2m+1's diagonal
+    }
+  };
+  store_tiles(std::integral_constant<int, ROLE>{});
+  if constexpr (FUSE) {
+    if (!to_slab) {
+      // The start runs on role 1 from its own accumulators (registers) and
+      // role 0's, dumped into the stage (free once both waves have passed
+      // the barrier behind the last half): the same tiles and the same
+      // acc_matvec arithmetic as the one-wave kernel, so the start is
+      // bitwise its start.  (Reading the tiles back from the stored tri16
+      // G instead -- 4 strided loads per tile per pass -- cost 3 x the
+      // one-wave kernel's start.)
+      start_stage<NB, USER, 4>(cacc, sacc, 4 * role, k, sc);
+#if MR_PAIR_SPLIT_START
+      // Split start: each wave takes the products of ITS tiles (from its
+      // registers) and role 1 adds role 0's partial result to its own
+      // (y = y0 + y1): both waves work, no tile dump -- but a summation
+      // order of its own, so the start is not bitwise the one-wave kernel's.
+      // Role 0's row partials / column sums / partial y live in the stage.
+      constexpr int NV = 2;
+      double (*partR0)[64] = reinterpret_cast<double (*)[64]>(stg);
+      double* yC0 = reinterpret_cast<double*>(stg) + 32 * 64;
+      double* Y0 = yC0 + 16 * NB;
+      __syncthreads();   // both waves done with the stage
+      if constexpr (ROLE == 1) {
+        float xv[NB];
+        load_row_seg<NB>(xv, cs.x + (int64_t)went * ldk + NB * col);
+        start_stage_x<NB>(xv, sc);
+      }
+      __syncthreads();
+      auto own = [](int bi, int bj) { return pair_owner(bi, bj) == ROLE; };
+      auto mine = [&](int bi, int bj) {
+        floatx4 t = acc[pair_local(bi, bj)];
+        asm volatile("" : "+v"(t));   // converted afresh in each pass
+        return t;
+      };
+      double yo[NV], pn[NV], pb = 0.0;
+      const float xbv = (USER && ROLE == 1) ? cs.xb[went] : 0.f;
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass) {
+        acc_matvec_g<NB, true>(mine, own, sc, ROLE == 0 ? partR0 : sc.partR,
+                               ROLE == 0 ? yC0 : sc.yC, k, yo);
+        if constexpr (ROLE == 0) {
+#pragma unroll
+          for (int h = 0; h < NV; ++h) Y0[lane + 64 * h] = yo[h];
+        }
+        __syncthreads();
+        if constexpr (ROLE == 1) {
+#pragma unroll
+          for (int h = 0; h < NV; ++h) yo[h] = Y0[lane + 64 * h] + yo[h];
+          if (pass == 0) start_r0<NB, USER>(yo, wt, (float)wlen, xbv, went, k, ldk, cs, sc, drr, pn, pb);
+          else start_q0<NB, USER>(yo, (float)wlen, pb, pn, went, k, ldk, cs, sc, dpq, dqq);
+        }
+        __syncthreads();   // p0 in sc.pv before the second pass
+      }
+#else
+      floatx4* dump = reinterpret_cast<floatx4*>(stg);
+      __syncthreads();   // both waves done with the stage
+      if constexpr (ROLE == 0) {
+#pragma unroll
+        for (int t = 0; t < PAIR_T; ++t) dump[t * 64 + lane] = acc[t];
+      } else {
+        float xv[NB];
+        load_row_seg<NB>(xv, cs.x + (int64_t)went * ldk + NB * col);
+        start_stage_x<NB>(xv, sc);
+      }
+      __syncthreads();
+      if constexpr (ROLE == 1) {
+        const float xbv = USER ? cs.xb[went] : 0.f;
+        start_from_tiles<NB, USER, true>(
+            [&](int bi, int bj) {
+              floatx4 t = pair_owner(bi, bj) == 1 ? acc[pair_local(bi, bj)]
+                                                  : dump[pair_local(bi, bj) * 64 + lane];
+              // opaque per call: the two acc_matvec passes convert the tiles
+              // afresh instead of the compiler keeping (spilling) the fp64
+              // copies of the first pass for the second
+              asm volatile("" : "+v"(t));
+              return t;
+            },
+            wt, (float)wlen, xbv, went, k, ldk, cs, sc, drr, dpq, dqq);
+      }
+#endif
+    }
+    if (cs.xbins) {   // one-pass CG: the entity's start sums, order-independent
+      const int64_t t3[3] = {xterm(drr, lane), xterm(dpq, lane), xterm(dqq, lane)};
+      xsum_flush<3>(t3, cs.xbins);
+    } else {
+      store_start_sums(drr, dpq, dqq, cs.parts);
+    }
+  }
+}
+
+template <bool USER, bool FUSE, bool BUF, bool RHSM>
+__global__ __launch_bounds__(128, 2) void gram_pair_kernel(
+    const WorkItem* __restrict__ work, int64_t n_work,
+    const int32_t* __restrict__ idx, const float* __restrict__ val,
+    const float* __restrict__ F, const float* __restrict__ bias, int k, int ldk, int zrow,
+    GramDst direct, GramDst slab, CgStart cs) {
+  __shared__ u32x4_t stg[PAIR_STAGE];
+  __shared__ StartScratch<8> sc;   // role 1's (the start runs on one wave)
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0)
+    gram_pair_wave<0, USER, FUSE, BUF, RHSM>(work, n_work, idx, val, F, bias, k, ldk, zrow,
+                                             direct, slab, cs, stg, sc);
+  else
+    gram_pair_wave<1, USER, FUSE, BUF, RHSM>(work, n_work, idx, val, F, bias, k, ldk, zrow,
+                                             direct, slab, cs, stg, sc);
+}
+
 // Split entities: the CG start after slab_reduce (one wave per entity).
 // the folded CG_START control, run by wave 0 of cg_start_split's last block
 // (defined with the control kernel below)
@@ -1428,8 +1978,29 @@ static int launch_gram_nb(hipStream_t s, bool user_side, int k, const WorkItem* 
                           const float* F, const float* bias, int zrow, GramDst direct,
                           GramDst slab, const CgStart* start, bool rhs_mfma) {
   if (n_work <= 0) return 0;
-  const int64_t grid = (n_work + GRAM_WAVES - 1) / GRAM_WAVES;
   const CgStart cs = start ? *start : CgStart{};
+  if constexpr (NB == 8 && MR_GRAM_PAIR) {   // one work item per pair of waves
+    const bool buf = (int64_t)(zrow + 1) * ldk_of(k) * 4 < ((int64_t)1 << 31);
+#define MR_GP(U, FU, B, R)                                                                     \
+  MR_LAUNCH((gram_pair_kernel<U, FU, B, R>), dim3((unsigned)n_work), dim3(128), 0, s, work,    \
+            n_work, idx, val, F, bias, k, ldk_of(k), zrow, direct, slab, cs)
+#define MR_GP_B(U, FU, R) \
+  if (buf) MR_GP(U, FU, true, R); else MR_GP(U, FU, false, R);
+    if (user_side) {
+      if (rhs_mfma) {
+        if (start) { MR_GP_B(true, true, true) } else { MR_GP_B(true, false, true) }
+      } else {
+        if (start) { MR_GP_B(true, true, false) } else { MR_GP_B(true, false, false) }
+      }
+    } else {
+      if (start) { MR_GP_B(false, true, false) } else { MR_GP_B(false, false, false) }
+    }
+#undef MR_GP_B
+#undef MR_GP
+    MR_HIP(hipGetLastError());
+    return 0;
+  }
+  const int64_t grid = (n_work + GRAM_WAVES - 1) / GRAM_WAVES;
   // buffer-resource gathers when the whole table (zrow + 1 rows) is < 2 GiB
   // and the row segment is whole dwordx4s (NB = 4, 8)
   constexpr bool BUFOK = NB % 4 == 0;

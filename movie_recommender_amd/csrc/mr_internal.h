@@ -274,7 +274,15 @@ int launch_gram(hipStream_t s, bool user_side, int k, const WorkItem* work,
                 int64_t n_work, const int32_t* idx, const float* val,
                 const float* F, const float* bias, int zrow, GramDst direct,
                 GramDst slab, const CgStart* start = nullptr, bool rhs_mfma = false);
-inline int64_t gram_blocks(int64_t n_work) { return (n_work + 3) / 4; }
+// Gram blocks of a launch over n_work work items: four one-wave items per
+// block, or (k = 113 ... 128, MR_GRAM_PAIR) one item per pair-of-waves block
+#ifndef MR_GRAM_PAIR
+#define MR_GRAM_PAIR 1
+#endif
+inline bool gram_pair_of(int k) { return MR_GRAM_PAIR && k > 112 && k <= 128; }
+inline int64_t gram_blocks(int64_t n_work, int k) {
+  return gram_pair_of(k) ? n_work : (n_work + 3) / 4;
+}
 int launch_cg_start_split(hipStream_t s, bool user_side, int k, const SplitItem* split,
                           int64_t n_split, GramDst direct, const CgStart& cs, double* parts,
                           const StartFold& fold = StartFold{});

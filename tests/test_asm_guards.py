@@ -6,11 +6,14 @@ A scheduling or compiler change that moved an accumulator read or a VALU
 write next to the MFMAs would make wrong normal equations without a fault;
 this check fails the build instead.
 
-For every gram_kernel<NB >= 5> instance:
+For every gram_kernel<NB >= 5> instance (and every gram_pair_kernel, whose
+accumulators are VGPRs: there the exit check is that each role's last MFMA
+run is followed at once by the 20 wait states of mfma_exit_guard_v):
   * every run of consecutive v_mfma instructions (s_nop pads between them
-    allowed) is entered through an s_nop of >= 3 wait states (the guard's
-    `s_nop 4`; VALU writes of P / the zeroed accumulators -> SrcA/B/C need
-    <= 2);
+    allowed) is entered >= 3 wait states after the last VALU instruction
+    (the guard's `s_nop 4`, or LDS loads / waits of the pair kernel's
+    partner operands; VALU writes of P / the zeroed accumulators ->
+    SrcA/B/C need <= 2);
   * no v_accvgpr_read / write inside a run (the accumulators stay pinned);
   * between the last v_mfma and the first later instruction touching the
     accumulators (v_accvgpr_read, or an AGPR source), >= 12 wait states on
@@ -84,14 +87,16 @@ def _backward(ins):
                     reason="library or llvm-objdump missing")
 def test_gram_mfma_wait_state_guards(tmp_path):
     checked = 0
+    checked_pair = []
     for j, obj in enumerate(_gfx950_objects(SO)):
         path = tmp_path / f"co{j}.o"
         path.write_bytes(obj)
         asm = subprocess.run([f"{LLVM}/llvm-objdump", "-d", str(path)], capture_output=True,
                              text=True).stdout
         for name, lines in _functions(asm).items():
+            pair = "gram_pair_kernel" in name
             m = re.search(r"gram_kernelILi(\d+)E", name)
-            if not m or int(m.group(1)) < 5:
+            if not pair and (not m or int(m.group(1)) < 5):
                 continue
             ins = [l.split(None, 1)[1] if re.match(r"^[0-9a-f]+:?\s", l) else l
                    for l in lines if l and not l.endswith(":")]
@@ -106,8 +111,28 @@ def test_gram_mfma_wait_state_guards(tmp_path):
                 else:
                     runs.append([t, t])
             for a, b in runs:
-                assert _nop_states(ins[a - 1]) >= 3, (name, ins[a - 3:a + 1])
+                # >= 3 wait states between the last VALU instruction (a
+                # VGPR writer) and the run: the guard's nops, or (the pair
+                # kernel's partner operands) LDS loads / waits, which write
+                # no VGPR by VALU and count one state each
+                states, t = 0, a - 1
+                while states < 3 and t >= 0:
+                    i = ins[t]
+                    if i.startswith("v_") and not i.startswith("v_mfma"):
+                        break
+                    states += _nop_states(i) or 1
+                    t -= 1
+                assert states >= 3, (name, ins[a - 4:a + 1])
                 assert not any("accvgpr" in i for i in ins[a:b + 1]), name
+            if pair:
+                # VGPR accumulators (no AGPR reads to find): each role's last
+                # MFMA is followed at once by mfma_exit_guard_v's 20 wait
+                # states, which take every accumulator as an operand
+                exits = [b for a, b in runs
+                         if [_nop_states(i) for i in ins[b + 1:b + 4]] == [8, 8, 4]]
+                assert len(exits) >= 2, (name, [ins[b + 1:b + 4] for a, b in runs][-4:])
+                checked_pair.append(name)
+                continue
             last = mf[-1]
             nxt = next(t for t in range(last + 1, len(ins))
                        if "accvgpr" in ins[t] or re.search(r"\ba\d+|\ba\[", ins[t]))
@@ -119,3 +144,6 @@ def test_gram_mfma_wait_state_guards(tmp_path):
             assert states >= 12, (name, ins[last + 1:nxt + 1])
             checked += 1
     assert checked >= 16     # NB = 5..8 x user/item x fused/unfused (x buffer forms)
+    # the NB = 8 pair kernel: user (rhs on MFMA or VALU) / item x fused /
+    # unfused x buffer forms
+    assert len(checked_pair) >= 12, checked_pair

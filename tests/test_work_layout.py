@@ -72,3 +72,41 @@ def test_small_tables_are_not_placed():
     _, _, _, same = expected_layout(ids, other, r, E, chunk=chunk,
                                     xcd_table_bytes=16 << 20, k=64, n_other=n_other)
     assert base == same
+
+
+def pair_pos(b, n):
+    """Host restatement of kernels.hip pair_pos: the work-list position of
+    block b of the NB = 8 pair Gram (one work item per 128-thread block)."""
+    if b >= (n & ~31):
+        return b
+    return 32 * (b >> 5) + 4 * (b & 7) + ((b >> 3) & 3)
+
+
+def test_pair_gram_block_placement():
+    """The pair Gram keeps the work list's XCD placement: block b runs on XCD
+    b mod 8 (dispatch round-robin) and takes the position p the list dealt
+    to XCD (p // 4) % 8, for every block of a full group of 32; the mapping
+    is a bijection on [0, n) for every n (the tail keeps p = b)."""
+    for n in (1, 31, 32, 33, 64, 100, 1000, 4097):
+        ps = [pair_pos(b, n) for b in range(n)]
+        assert sorted(ps) == list(range(n)), n
+        full = n & ~31
+        assert all((ps[b] // 4) % 8 == b % 8 for b in range(full)), n
+
+
+def test_pair_gram_block_partition():
+    """The 36 upper 16 x 16 blocks at NB = 8 split 18 / 18 between the pair's
+    waves (kernels.hip pair_owner / pair_local): role 0 the blocks inside
+    segments 0-3 and (bi <= 3, bj in {4, 5}), role 1 the rest; each role's
+    folded diagonal pairs (2m, 2m + 1) are its own."""
+    def owner(bi, bj):
+        return 0 if (bi <= 3 and bj <= 5) else 1
+
+    blocks = [(bi, bj) for bi in range(8) for bj in range(bi, 8)]
+    assert sum(owner(*b) == 0 for b in blocks) == 18 == sum(owner(*b) == 1 for b in blocks)
+    for m in range(4):
+        assert owner(2 * m, 2 * m) == owner(2 * m + 1, 2 * m + 1) == (0 if m < 2 else 1)
+    # partner segments each role reads: role 0 only 4, 5; role 1 only 0-3
+    need0 = {s for (bi, bj) in blocks if owner(bi, bj) == 0 for s in (bi, bj)} - {0, 1, 2, 3}
+    need1 = {s for (bi, bj) in blocks if owner(bi, bj) == 1 for s in (bi, bj)} - {4, 5, 6, 7}
+    assert need0 == {4, 5} and need1 == {0, 1, 2, 3}
