@@ -187,9 +187,20 @@ struct CgLs {
     std::vector<int64_t> offa(rows + 1), offt(cols + 1);
     MR_D2H(offa.data(), rp, (rows + 1) * 8, s);
     MR_D2H(offt.data(), tp, (cols + 1) * 8, s);
-    const std::vector<int64_t> ba = row_blocks(offa), bt = row_blocks(offt);
-    n_blk_a = (int64_t)ba.size() - 1;
-    n_blk_t = (int64_t)bt.size() - 1;
+    // uploaded as (first row, its first non-zero) pairs: the kernels read a
+    // block's bounds with no dependent load through the row offsets
+    auto pairs = [](const std::vector<int64_t>& bl, const std::vector<int64_t>& off) {
+      std::vector<int64_t> pr(2 * bl.size());
+      for (size_t i = 0; i < bl.size(); ++i) {
+        pr[2 * i] = bl[i];
+        pr[2 * i + 1] = off[bl[i]];
+      }
+      return pr;
+    };
+    const std::vector<int64_t> ba = pairs(row_blocks(offa), offa),
+                               bt = pairs(row_blocks(offt), offt);
+    n_blk_a = (int64_t)ba.size() / 2 - 1;
+    n_blk_t = (int64_t)bt.size() / 2 - 1;
     if (dmalloc(&blk_a, (int64_t)ba.size(), owned) || dmalloc(&blk_t, (int64_t)bt.size(), owned))
       return -1;
     MR_H2D(blk_a, ba.data(), ba.size() * 8, s);

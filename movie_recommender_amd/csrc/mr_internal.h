@@ -362,8 +362,9 @@ int launch_predict(hipStream_t s, int64_t n, int k, int ldk, const int* uid,
                    const int* iid, const float* Ufac, const float* Ubias,
                    const float* Vfac, double* out);
 // General CSR (fp64) CG least squares (cg_least_squares_from_python):
-// CSR-stream SpMV over row blocks blk[0..n_blk] (consecutive rows with
-// <= 2048 non-zeros, <= 256 rows, or one longer row), fixed grid of
+// CSR-stream SpMV over row blocks b = 0..n_blk-1 (consecutive rows with
+// <= 2048 non-zeros, <= 256 rows, or one longer row; blk[2b] = first row,
+// blk[2b+1] = its first non-zero, n_blk + 1 pairs), fixed grid of
 // min(n_blk, n_part) workgroups.  The CG's r and p live interleaved, rp[2j]
 // = r_j, rp[2j+1] = p_j (one 16-byte gather per non-zero).  gather SPG_X:
 // x_c = xa[c]; SPG_P: p_c = -r_c + beta p_c from xa = rp; SPG_P0: p_c from
