@@ -1225,6 +1225,16 @@ __device__ __forceinline__ void bf3_mfma(floatx4 (&acc)[NB * (NB + 1) / 2], floa
   }
 }
 
+// Stores of the Gram's tri16 G (MR_G_NT: non-temporal, so the stream of G
+// does not evict the gathered factor table from the Infinity Cache)
+#ifndef MR_G_NT
+#define MR_G_NT 1
+#endif
+__device__ __forceinline__ void gst(float* p, float v) {
+  if (MR_G_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 template <int NB, bool USER, bool FUSE, bool BUF>
 __device__ __forceinline__ void gram_wave(
     int64_t wi, const WorkItem* __restrict__ work,
@@ -1398,7 +1408,7 @@ __device__ __forceinline__ void gram_wave(
     for (int bj = bi + 1; bj < NB; ++bj) {
       const int t = acc_tile(bi, bj, NB), o = off_index(bi, bj, NB) * 256;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) Gl[o + 16 * r] = acc[t][r];
+      for (int r = 0; r < 4; ++r) gst(&Gl[o + 16 * r], acc[t][r]);
     }
   }
 #pragma unroll
@@ -1408,15 +1418,15 @@ __device__ __forceinline__ void gram_wave(
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = 4 * q + r;
-      Gl[(NO + m) * 256 + 16 * r] = col >= row ? acc[te][r] : acc[to][r];
+      gst(&Gl[(NO + m) * 256 + 16 * r], col >= row ? acc[te][r] : acc[to][r]);
       if (col - 4 * q == r) dg = acc[to][r];
     }
-    if ((col >> 2) == q) Gd[NTILE * 256 + m * 16 + col] = dg;   // D_2m+1's diagonal
+    if ((col >> 2) == q) gst(&Gd[NTILE * 256 + m * 16 + col], dg);   // D_2m+1's diagonal
   }
   if constexpr ((NB & 1) != 0) {
     const int t = acc_tile(NB - 1, NB - 1, NB);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) Gl[(NO + NF) * 256 + 16 * r] = acc[t][r];
+    for (int r = 0; r < 4; ++r) gst(&Gl[(NO + NF) * 256 + 16 * r], acc[t][r]);
   }
   if constexpr (FUSE) {
     if (!to_slab)
@@ -1676,6 +1686,16 @@ __device__ __forceinline__ void gram_pair_wave(
   const int q = lane >> 4, col = lane & 15;
   const int64_t end = wbeg + wlen;
   constexpr uint32_t row_bytes = 64u * NB;
+  // fused start (role 1): this entity's x segment and bias, fetched now and
+  // used after the halves (at the epilogue they were an exposed global load
+  // per work item)
+  float xpre[NB];
+  float xbpre = 0.f;
+  if constexpr (FUSE && ROLE == 1) {
+    const int64_t xe = wslab < 0 ? (int64_t)went : 0;
+    load_row_seg<NB>(xpre, cs.x + xe * ldk + NB * col);
+    if (USER) xbpre = cs.xb[xe];
+  }
   // this wave's 4 segments: floats 4 role .. 4 role + 3 of the lane's 8
   RowSrc src;
   src.Fc = reinterpret_cast<const char*>(F) + 4 * NB * col + 16 * role;
@@ -1811,7 +1831,7 @@ __device__ __forceinline__ void gram_pair_wave(
         if (pair_owner(bi, bj) != decltype(own)::value) continue;
         const int t = pair_local(bi, bj), o = off_index(bi, bj, NB) * 256;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Gl[o + 16 * r] = acc[t][r];
+        for (int r = 0; r < 4; ++r) gst(&Gl[o + 16 * r], acc[t][r]);
       }
     }
 #pragma unroll
@@ -1821,10 +1841,10 @@ __device__ __forceinline__ void gram_pair_wave(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = 4 * q + r;
-        Gl[(NO + m) * 256 + 16 * r] = col >= row ? acc[te][r] : acc[to][r];
+        gst(&Gl[(NO + m) * 256 + 16 * r], col >= row ? acc[te][r] : acc[to][r]);
         if (col - 4 * q == r) dg = acc[to][r];
       }
-      if ((col >> 2) == q) Gd[NTILE * 256 + m * 16 + col] = dg;   // D_2m+1's diagonal
+      if ((col >> 2) == q) gst(&Gd[NTILE * 256 + m * 16 + col], dg);   // D_2m+1's diagonal
     }
   };
   store_tiles(std::integral_constant<int, ROLE>{});
@@ -1849,11 +1869,7 @@ __device__ __forceinline__ void gram_pair_wave(
       double* yC0 = reinterpret_cast<double*>(stg) + 32 * 64;
       double* Y0 = yC0 + 16 * NB;
       __syncthreads();   // both waves done with the stage
-      if constexpr (ROLE == 1) {
-        float xv[NB];
-        load_row_seg<NB>(xv, cs.x + (int64_t)went * ldk + NB * col);
-        start_stage_x<NB>(xv, sc);
-      }
+      if constexpr (ROLE == 1) start_stage_x<NB>(xpre, sc);
       __syncthreads();
       auto own = [](int bi, int bj) { return pair_owner(bi, bj) == ROLE; };
       auto mine = [&](int bi, int bj) {
@@ -1862,7 +1878,7 @@ __device__ __forceinline__ void gram_pair_wave(
         return t;
       };
       double yo[NV], pn[NV], pb = 0.0;
-      const float xbv = (USER && ROLE == 1) ? cs.xb[went] : 0.f;
+      const float xbv = (USER && ROLE == 1) ? xbpre : 0.f;
 #pragma unroll
       for (int pass = 0; pass < 2; ++pass) {
         acc_matvec_g<NB, true>(mine, own, sc, ROLE == 0 ? partR0 : sc.partR,
@@ -1887,13 +1903,11 @@ __device__ __forceinline__ void gram_pair_wave(
 #pragma unroll
         for (int t = 0; t < PAIR_T; ++t) dump[t * 64 + lane] = acc[t];
       } else {
-        float xv[NB];
-        load_row_seg<NB>(xv, cs.x + (int64_t)went * ldk + NB * col);
-        start_stage_x<NB>(xv, sc);
+        start_stage_x<NB>(xpre, sc);
       }
       __syncthreads();
       if constexpr (ROLE == 1) {
-        const float xbv = USER ? cs.xb[went] : 0.f;
+        const float xbv = USER ? xbpre : 0.f;
         start_from_tiles<NB, USER, true>(
             [&](int bi, int bj) {
               floatx4 t = pair_owner(bi, bj) == 1 ? acc[pair_local(bi, bj)]
