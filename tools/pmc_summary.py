@@ -16,13 +16,15 @@ import os
 import re
 
 CLASSES = [
-    ("gram_users", r"gram_kernel<\d+, true"),
-    ("gram_items", r"gram_kernel<\d+, false"),
+    ("gram_users", r"gram_kernel<\d+, true|gram_pair_kernel<true"),
+    ("gram_items", r"gram_kernel<\d+, false|gram_pair_kernel<false"),
     ("matvec_users", r"(cg_matvec_kernel|cg_onepass_kernel)<\d+, true"),
     ("matvec_items", r"(cg_matvec_kernel|cg_onepass_kernel)<\d+, false"),
     ("slab_reduce", r"slab_reduce_kernel"),
     ("cg_update", r"cg_update_kernel"),
     ("cg_control", r"cg_control_kernel"),
+    ("rec_score", r"rec_score_kernel"),
+    ("rec_select", r"rec_select_kernel"),
 ]
 
 
