@@ -344,7 +344,7 @@ def main():
                          "(e.g. 0,0 puts two ranks on GPU 0; needs --comm gloo)")
     ap.add_argument("--pmc", default=None,
                     help="per-kernel HBM bytes from a rocprofv3 --pmc run (optional; default "
-                         "profiles/pmc_r04.json at k = 64, profiles/pmc_r04_k<k>.json otherwise)")
+                         "profiles/pmc_r05.json at k = 64, profiles/pmc_r05_k<k>.json otherwise; r04 if absent)")
     args = ap.parse_args()
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -621,8 +621,13 @@ def main():
         gather = {"bytes_per_launch": int(gb), "achieved_GBps": round(gb / avg_s / 1e9, 1),
                   "peak_GBps": GATHER_PEAK_GBS, "frac": round(gb / avg_s / 1e9 / GATHER_PEAK_GBS, 3)}
     traffic = None
-    pmc_path = args.pmc or os.path.join(
-        ROOT, "profiles", "pmc_r04.json" if k == 64 else f"pmc_r04_k{k}.json")
+    pmc_path = args.pmc
+    if not pmc_path:   # this round's counter passes, else the previous round's
+        for rnd in ("r05", "r04"):
+            pmc_path = os.path.join(ROOT, "profiles",
+                                    f"pmc_{rnd}.json" if k == 64 else f"pmc_{rnd}_k{k}.json")
+            if os.path.exists(pmc_path):
+                break
     if os.path.exists(pmc_path):
         with open(pmc_path) as f:
             pmc = json.load(f)
