@@ -1483,10 +1483,13 @@ __global__ __launch_bounds__(256, (NB <= 4 ? 3 : 1)) void gram_kernel(
 // same halves with the same six products in the same order, so G is
 // bitwise the one-wave kernel's.  Epilogue: each wave stores its own tiles
 // (role 0 holds the folded diagonal pairs 0-1 and 2-3, role 1 4-5 and 6-7);
-// the fused CG start runs on role 1 with role 0's tiles dumped into the
-// (then free) stage -- the same acc_matvec arithmetic, so the start is
-// bitwise the one-wave kernel's too.  Accumulators in VGPRs (mfma_acc), at
-// most 256 registers per wave: two waves per SIMD.
+// the fused CG start is split over the pair (each wave takes the products of
+// its own tiles, role 1 adds role 0's partials: a summation order of its
+// own), or with MR_PAIR_SPLIT_START = 0 runs on role 1 over role 0's tiles
+// dumped into the (then free) stage -- the one-wave kernel's acc_matvec
+// arithmetic, bitwise its start.  Role 1 fetches x at the wave's start.
+// Accumulators in VGPRs (mfma_acc), at most 256 registers per wave: two
+// waves per SIMD.
 // ---------------------------------------------------------------------------
 constexpr int PAIR_T = 18;   // upper blocks per wave
 // MR_PAIR_PREFETCH: the next half's rows are gathered while this half's
