@@ -26,9 +26,35 @@ def runs_of(dist, kind):
     return [r for r in dist["runs"] if r["kind"] == kind]
 
 
+def stratified_p(sample, pool, metric, n_perm=20000, seed=0):
+    """Seed-stratified permutation test (two-sided).
+
+    Null: within each initial-factor seed, the sample's run is exchangeable
+    with the reference's runs of THAT seed (its thread counts).  The pool's
+    runs are not independent draws -- the runs of one seed share their start
+    and the sample uses the same seeds -- so the permutation resamples within
+    seeds only: the statistic is the sum over seeds of the sample run's
+    centred mid-rank among that seed's m + 1 values, and its null
+    distribution picks, per seed, which of the m + 1 values is "the
+    sample's" (Monte Carlo, fixed generator: the p-value is reproducible)."""
+    from scipy.stats import rankdata
+    rng = np.random.default_rng(seed)
+    t_obs, null = 0.0, np.zeros(n_perm)
+    for s in sorted({r["seed"] for r in sample}):
+        x = [r[metric] for r in sample if r["seed"] == s]
+        ys = [r[metric] for r in pool if r["seed"] == s]
+        assert len(x) == 1 and ys, (s, len(x), len(ys))
+        rk = rankdata(np.array(x + ys, np.float64))
+        rk -= rk.mean()
+        t_obs += rk[0]
+        null += rk[rng.integers(0, len(rk), n_perm)]
+    return float((np.sum(np.abs(null) >= abs(t_obs) - 1e-9) + 1) / (n_perm + 1))
+
+
 def compare(sample, pool, metrics=METRICS):
-    """{metric: (mean sample, mean pool, Mann-Whitney p, KS p)} -- two-sided
-    tests of ``sample`` (list of dicts) against ``pool`` (list of dicts)."""
+    """{metric: (mean sample, mean pool, Mann-Whitney p, KS p, seed-
+    stratified permutation p)} -- two-sided tests of ``sample`` (list of
+    dicts, one run per seed) against ``pool`` (list of dicts)."""
     from scipy.stats import ks_2samp, mannwhitneyu
     out = {}
     for m in metrics:
@@ -36,17 +62,39 @@ def compare(sample, pool, metrics=METRICS):
         y = np.array([r[m] for r in pool], np.float64)
         out[m] = (float(x.mean()), float(y.mean()),
                   float(mannwhitneyu(x, y, alternative="two-sided").pvalue),
-                  float(ks_2samp(x, y).pvalue))
+                  float(ks_2samp(x, y).pvalue),
+                  stratified_p(sample, pool, m))
     return out
 
 
 def describe(res):
-    return "; ".join(f"{m} {a:.4f} vs {b:.4f} (MW p={p:.3f}, KS p={q:.3f})"
-                     for m, (a, b, p, q) in res.items())
+    return "; ".join(f"{m} {a:.4f} vs {b:.4f} (MW p={p:.3f}, KS p={q:.3f}, strat p={s:.4f})"
+                     for m, (a, b, p, q, s) in res.items())
+
+
+def holm_rejects(pvals, alpha=P_MIN):
+    """Holm's step-down procedure over the metrics (family-wise error
+    ``alpha``): the metrics whose null is rejected."""
+    order = sorted(pvals, key=pvals.get)
+    out = []
+    for j, m in enumerate(order):
+        if pvals[m] >= alpha / (len(order) - j):
+            break
+        out.append(m)
+    return out
 
 
 def failing(res, p_min=P_MIN):
-    return {m: v for m, v in res.items() if v[2] < p_min}
+    """Two gates: (1) the two-sided Mann-Whitney of the sample against the
+    whole pool at p >= p_min per metric (VERDICT r04/r05's test; it treats the
+    pool's runs as independent, which they are not -- see stratified_p); (2)
+    the seed-stratified permutation test with Holm's correction across the
+    metrics (family-wise p_min): the calibrated one.  Returns the metrics
+    failing either gate."""
+    bad = {m: v for m, v in res.items() if v[2] < p_min}
+    for m in holm_rejects({m: v[4] for m, v in res.items()}, p_min):
+        bad[m] = res[m]
+    return bad
 
 
 def seed_ranges(pool, metric):

@@ -21,7 +21,11 @@ Fixtures
                                  thread counts {1,2,3,4,6,8} (+ the oracle's
                                  block restatement per seed), for the
                                  two-sample realistic-data test
-  G5  als_edge_*.npz, cg_edge_sparse.npz   max_iteration 0..4, zero ratings,
+  G13 dist_mlfull_k64.json       the same at the headline config (ML-full
+                                 shape, k = 64, the reference's own outer
+                                 stop): 20 seeds x thread counts {1, 2, 4}
+                                 (``g13 <tc>`` per process, then ``g13m``)
+  G5 als_edge_*.npz, cg_edge_sparse.npz   max_iteration 0..4, zero ratings,
                                  duplicate pairs, empty CSR rows / columns
 """
 import json
@@ -542,6 +546,13 @@ def g12(n_seeds=32):
     precision emulation (``block64`` / ``block32``), so the test can place
     the GPU's per-seed sample against both."""
     tcs = (1, 2, 3, 4, 6, 8)
+    try:
+        _g12(n_seeds, tcs)
+    finally:
+        ref.set_thread_count(1)
+
+
+def _g12(n_seeds, tcs):
     for k in (10, 32):
         rs_ = synth.movielens_like("ml-100k", k, seed=synth.DATA_SEED, test_ratio=0.2)
         runs = []
@@ -566,10 +577,77 @@ def g12(n_seeds=32):
                     thread_counts=list(tcs), n_seeds=n_seeds, runs=runs, meta=_meta(None))
         with open(os.path.join(HERE, f"dist_ml100k_k{k}.json"), "w") as f:
             json.dump(dist, f, indent=0)
+
+
+G13_TCS = (1, 2, 4)
+G13_SEEDS = 20
+
+
+def _g13_part(tc):
+    return os.path.join("/tmp", f"dist_mlfull_k64_tc{tc}.partial.json")
+
+
+def g13(tc=None):
+    """Round 6 (VERDICT r05 "do this" 2): the headline config's realistic-
+    data distribution.  The ML-full-shaped generator at k = 64 (20 % held
+    out, the data of ``g9``), initial-factor seeds 0 .. 19, the compiled
+    reference with ITS OWN outer stop (``max_iteration`` = 200, the stop test
+    of ``matrix.cpp:871-875``) at thread counts {1, 2, 4}.  One process per
+    thread count (``make_golden.py g13 <tc>``; a run holds ~13 GB of design
+    matrices), results appended per run to a partial file so an interrupted
+    generation resumes; ``g13m`` merges them into ``dist_mlfull_k64.json``."""
+    tcs = G13_TCS if tc is None else (int(tc),)
+    k = 64
+    rs_ = synth.movielens_like("ml-full", k, seed=synth.DATA_SEED, test_ratio=0.2)
+    for t in tcs:
+        part = _g13_part(t)
+        runs = json.load(open(part)) if os.path.exists(part) else []
+        done = {r["seed"] for r in runs}
+        ref.set_thread_count(t)
+        for seed in range(G13_SEEDS):
+            if seed in done:
+                continue
+            U0, V0 = ref.init_factors(rs_.num_users, rs_.num_items, k, seed)
+            t0 = __import__("time").perf_counter()
+            U, V, ret = ref.als(rs_.user_ids, rs_.item_ids, rs_.ratings, k, U0, V0)
+            wall = __import__("time").perf_counter() - t0
+            runs.append(dict(kind="ref", seed=seed, tc=t, ret=ret, wall_s=round(wall, 1),
+                             **_quality(U, V, k, rs_)))
+            print("G13", runs[-1], flush=True)
+            with open(part, "w") as f:
+                json.dump(runs, f)
     ref.set_thread_count(1)
 
 
+def g13m():
+    k = 64
+    rs_ = synth.movielens_like("ml-full", k, seed=synth.DATA_SEED, test_ratio=0.2)
+    runs = []
+    for t in G13_TCS:
+        runs += json.load(open(_g13_part(t)))
+    runs.sort(key=lambda r: (r["seed"], r["tc"]))
+    assert len(runs) == G13_SEEDS * len(G13_TCS), len(runs)
+    dist = dict(shape="ml-full", k=k, data_seed=synth.DATA_SEED, test_ratio=0.2,
+                max_iteration=200, n_train=int(rs_.n), n_test=int(len(rs_.test_ratings)),
+                num_users=rs_.num_users, num_items=rs_.num_items,
+                ratings_checksum=float(np.sum(rs_.ratings)),
+                medians_checksum=float(np.sum(rs_.medians)),
+                thread_counts=list(G13_TCS), n_seeds=G13_SEEDS, runs=runs, meta=_meta(None))
+    with open(os.path.join(HERE, "dist_mlfull_k64.json"), "w") as f:
+        json.dump(dist, f, indent=0)
+
+
 if __name__ == "__main__":
-    steps = sys.argv[1:] or ["g1", "g2", "g3", "g4", "g5", "g6", "g7", "g8"]
-    for s in steps:
-        globals()[s]()
+    # default: the fixtures every test reads (g4, g8, g9 are superseded:
+    # band_ml100k_k10.json is gone, g12 / g13 write the distributions, and
+    # g13 runs per thread count: ``g13 1``, ``g13 2``, ``g13 4``, then ``g13m``)
+    args = sys.argv[1:] or ["g1", "g2", "g3", "g5", "g6", "g7", "g10", "g11", "g12"]
+    i = 0
+    while i < len(args):
+        fn = globals()[args[i]]
+        if args[i] == "g13" and i + 1 < len(args) and args[i + 1].isdigit():
+            fn(args[i + 1])
+            i += 2
+        else:
+            fn()
+            i += 1

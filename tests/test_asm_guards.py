@@ -76,6 +76,17 @@ def _nop_states(ins):
     return int(m.group(1), 0) + 1 if m else 0
 
 
+def _vregs(ops):
+    """Set of VGPR numbers named in an operand string (v7, v[8:11])."""
+    out = set()
+    for lo, hi, one in re.findall(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b", ops):
+        if one:
+            out.add(int(one))
+        else:
+            out |= set(range(int(lo), int(hi) + 1))
+    return out
+
+
 def _backward(ins):
     # llvm-objdump prints a branch target as a signed 16-bit word offset
     # (e.g. `s_cbranch_scc0 64781` = -755): >= 0x8000 jumps back
@@ -131,6 +142,32 @@ def test_gram_mfma_wait_state_guards(tmp_path):
                 exits = [b for a, b in runs
                          if [_nop_states(i) for i in ins[b + 1:b + 4]] == [8, 8, 4]]
                 assert len(exits) >= 2, (name, [ins[b + 1:b + 4] for a, b in runs][-4:])
+                assert exits[-1] == runs[-1][1], (name, "last MFMA run unguarded")
+                # per run: the first later non-MFMA instruction that touches a
+                # register the run wrote comes >= 12 wait states after it on
+                # the straight-line path (8-pass XDL result -> VALU / VMEM /
+                # LDS reader), or a later MFMA run takes over (XDL -> XDL
+                # srcC forwarding); a run may not be left by a forward branch
+                # before its results are safe (a role's last run is followed
+                # by the guard, whichever role's code comes after it)
+                for a, b in runs:
+                    dst = set()
+                    for i in ins[a:b + 1]:
+                        if i.startswith("v_mfma"):
+                            dst |= _vregs(i.split(None, 1)[1].split(",")[0])
+                    states = 0
+                    for t in range(b + 1, len(ins)):
+                        i = ins[t]
+                        if i.startswith("v_mfma"):
+                            break
+                        if re.match(r"s_(c)?branch", i) and not _backward(i):
+                            assert states >= 12, (name, "forward branch", ins[b:t + 1])
+                            break
+                        if (i.startswith(("v_", "ds_", "global_", "buffer_", "flat_"))
+                                and " " in i and _vregs(i.split(None, 1)[1]) & dst):
+                            assert states >= 12, (name, ins[b:t + 1])
+                            break
+                        states += _nop_states(i) or 1
                 checked_pair.append(name)
                 continue
             last = mf[-1]

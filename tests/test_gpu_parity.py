@@ -264,7 +264,7 @@ def test_cg_sweep_direction_is_bitwise_neutral(gpu, k):
 
 
 @pytest.mark.parametrize("ratings", ["normal", "halfstar"])
-@pytest.mark.parametrize("k", [3, 10, 16, 20, 32, 33, 64, 65, 96, 128, 144, 200, 300])
+@pytest.mark.parametrize("k", [3, 10, 16, 20, 32, 33, 64, 65, 96, 120, 128, 144, 200, 300])
 def test_gram_kernel_vs_numpy(gpu, k, ratings):
     """Normal equations of both sides against fp64 NumPy -- VALU fp32 for
     k < 32, bf16x3 split on the bf16 MFMA for 32 <= k <= 128, the streamed
@@ -302,7 +302,7 @@ def test_gram_kernel_vs_numpy(gpu, k, ratings):
     _lib.check(_lib.lib().mr_set_gram_chunk(2048), "reset chunk")
 
 
-@pytest.mark.parametrize("k", [5, 10, 32, 33, 64, 65, 96, 112, 128, 144, 200, 300])
+@pytest.mark.parametrize("k", [5, 10, 32, 33, 64, 65, 96, 112, 120, 128, 144, 200, 300])
 @pytest.mark.parametrize("fuse,chunk,onepass", [(1, 2048, 1), (1, 64, 1), (0, 2048, 1),
                                                 (1, 2048, 0), (0, 2048, 0)])
 def test_cg_iterations_vs_oracle(gpu, k, fuse, chunk, onepass):
@@ -613,7 +613,7 @@ def test_band_headline_shape_heldout_rmse(gpu):
     # headline shape (5 GPU seeds against 30 reference runs: low power, but
     # the same two-sided test and threshold)
     import dist_stats as DS
-    sample = [{m: got[m][j] for m in got} for j in range(len(seeds))]
+    sample = [dict({m: got[m][j] for m in got}, seed=seeds[j]) for j in range(len(seeds))]
     res = DS.compare(sample, band["runs"])
     print("headline shape: " + DS.describe(res), flush=True)
     warnings.warn("headline-shape distribution: " + DS.describe(res))

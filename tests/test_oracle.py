@@ -139,14 +139,17 @@ def test_dist_reference_runs_reproduce():
     d = DS.load_dist(GOLDEN, 10)
     rs = synth.movielens_like(d["shape"], 10, seed=d["data_seed"], test_ratio=d["test_ratio"])
     U0, V0 = ref.init_factors(rs.num_users, rs.num_items, 10, 3)
-    for tc in (1, 4):
-        want = [r for r in DS.runs_of(d, "ref") if r["seed"] == 3 and r["tc"] == tc][0]
-        ref.set_thread_count(tc)
-        U, V, ret = ref.als(rs.user_ids, rs.item_ids, rs.ratings, 10, U0, V0)
-        assert ret == want["ret"]
-        assert O.rmse(U, V, rs.test_user_ids, rs.test_item_ids, rs.test_ratings, 10) == \
-            pytest.approx(want["test_rmse"], rel=1e-12)
-    ref.set_thread_count(1)
+    try:
+        for tc in (1, 4):
+            want = [r for r in DS.runs_of(d, "ref") if r["seed"] == 3 and r["tc"] == tc][0]
+            ref.set_thread_count(tc)
+            U, V, ret = ref.als(rs.user_ids, rs.item_ids, rs.ratings, 10, U0, V0)
+            assert ret == want["ret"]
+            assert O.rmse(U, V, rs.test_user_ids, rs.test_item_ids, rs.test_ratings, 10) == \
+                pytest.approx(want["test_rmse"], rel=1e-12)
+    finally:
+        # later tests assume the reference's default summation order
+        ref.set_thread_count(1)
 
 
 def test_exact_solve_matches_numpy_lstsq():
