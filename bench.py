@@ -52,6 +52,12 @@ HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_PEAK_TFS = 157.3        # MI355X FP32 vector / f32-MFMA dense peak
 GATHER_PEAK_GBS = 8600.0   # MI355X_MICROARCH.md: random rows, 38 MB table (Infinity Cache)
 METRIC = "ratings/sec per ALS iteration (MovieLens-full, k=64); RMSE parity"
+# collective model (DESIGN.md "Multi-GPU"): effective xGMI rate of one peer
+# link for the factor all-gather (each peer's block arrives over its own
+# link, in parallel) and the device latency of one peer all-reduce of the CG
+# scalars between GPUs
+XGMI_LINK_GBPS = 50.0
+PEER_REDUCE_US = 9.5
 
 
 def log(*a):
@@ -95,6 +101,9 @@ def algorithmic_cost(cls, k, n_users, n_items, n_ratings, ldk, fused=True, n_rat
     and writes p, r, q, x (6 x 8 + 2 x 4 B) instead of p rw, r read, q write
     (4 x 8 B); cg_update then only runs the finish pass once per solve (x +=
     alpha p: x rw fp32, p read)."""
+    if cls.startswith("resident_"):   # per CG iteration: the one-pass iteration's bytes
+        return algorithmic_cost("matvec_" + cls[len("resident_"):], k, n_users, n_items,
+                                n_ratings, ldk, fused, n_ratings_items, True)
     K = k + 1
     nb = (k + 15) // 16
     gsz = (nb * (nb - 1) // 2 + nb // 2 + nb % 2) * 256 + (nb // 2) * 16
@@ -262,6 +271,61 @@ def gpu_cg_rate(st, n_u, n_i):
             "ms_per_cg_iteration_items": round(si / ci, 4),
             "ratings_cg_iterations_per_s": round((n_u * cu + n_i * ci) / ((su + si) / 1e3), 1),
             "note": "solve phases of the instrumented replay; the Gram is not included"}
+
+
+def step_decomposition(st, steps, elapsed, ctx, k, world, dist, events_ms):
+    """Where a sharded step goes (VERDICT r05 "do this" 3), per rank from the
+    instrumented replay: the factor exchange (pack + all-gather + unstage,
+    kernel class ``exchange``), the device time the finalizing waves spent in
+    the peer all-reduce of the CG scalars (``peer_wait``: the reduction itself
+    plus the wait for the slowest rank), and everything else (the rank's own
+    Grams and CG).  ``model_step_ms`` is the collective model's prediction
+    for this run: the slowest rank's own compute + the all-gathers at
+    XGMI_LINK_GBPS per peer link + the peer reductions at PEER_REDUCE_US
+    each; beside it the measured step (max and min over ranks)."""
+    exch = st["kernel_ms"].get("exchange", 0.0) / steps
+    peer = st.get("peer_wait_ms", 0.0) / steps
+    n_red = st.get("peer_reductions", 0) / steps
+    busy = sum(v for c, v in st["kernel_ms"].items() if c != "exchange") / steps
+    # the rank's own compute: its kernels minus the time its finalizing waves
+    # spent in the peer reductions (inside the CG kernels)
+    own = max(0.0, busy - peer)
+    mine = {"step_ms": elapsed * 1e3 / steps,
+            "step_ms_with_kernel_events": events_ms, "compute_ms": own, "exchange_ms": exch,
+            "peer_wait_ms": peer, "peer_reductions": n_red}
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    ldk = (k + 15) // 16 * 16
+    _, nu, _ = ctx.local_size("users")
+    _, ni, _ = ctx.local_size("items")
+    rows = [None] * world
+    dist.all_gather_object(rows, (nu, ni))
+    max_u = max(r[0] for r in rows)
+    max_i = max(r[1] for r in rows)
+    # per half-step every rank receives world - 1 padded blocks, one per peer
+    # link in parallel: the largest block sets the time
+    ag_bytes = (max_u * (ldk + 1) + max_i * ldk) * 4.0
+    exch_model = ag_bytes / (XGMI_LINK_GBPS * 1e9) * 1e3 if world > 1 else 0.0
+    peer_model = max(r["peer_reductions"] for r in allr) * PEER_REDUCE_US / 1e3
+    compute = max(r["compute_ms"] for r in allr)
+    r3 = lambda x: round(x, 4)  # noqa: E731
+    return {"exchange_ms_per_step": r3(max(r["exchange_ms"] for r in allr)),
+            "peer_wait_ms_per_step": r3(max(r["peer_wait_ms"] for r in allr)),
+            "peer_reductions_per_step": r3(max(r["peer_reductions"] for r in allr)),
+            "compute_ms_per_step_by_rank": [r3(r["compute_ms"]) for r in allr],
+            "exchange_ms_per_step_by_rank": [r3(r["exchange_ms"]) for r in allr],
+            "peer_wait_ms_per_step_by_rank": [r3(r["peer_wait_ms"]) for r in allr],
+            "step_ms_max": r3(max(r["step_ms"] for r in allr)),
+            "step_ms_min": r3(min(r["step_ms"] for r in allr)),
+            "model_step_ms": r3(compute + exch_model + peer_model),
+            "model": {"compute_ms": r3(compute), "exchange_ms": r3(exch_model),
+                      "peer_reductions_ms": r3(peer_model),
+                      "allgather_bytes_per_peer_block": int(ag_bytes),
+                      "xgmi_link_GBps": XGMI_LINK_GBPS, "peer_reduce_us": PEER_REDUCE_US,
+                      "how": ("compute = the slowest rank's own kernel time per step (its "
+                              "replay's kernel table minus exchange and peer-reduction time); "
+                              "all-gathers of the largest shard's rows at the link rate; "
+                              "peer reductions at the xGMI latency (DESIGN.md Multi-GPU)")}}
 
 
 def free_port():
@@ -501,7 +565,8 @@ def main():
         st_ev = ctx.stats()
         replay_identical = (st_ev["cg_users_total"] == st["cg_users_total"]
                             and st_ev["cg_items_total"] == st["cg_items_total"])
-        for key in ("kernel_ms", "kernel_launches", "phase_ms"):
+        for key in ("kernel_ms", "kernel_launches", "kernel_units", "phase_ms", "peer_wait_ms",
+                    "peer_reductions"):
             st[key] = st_ev[key]
     elif instrument:
         events_ms = elapsed * 1e3 / args.steps
@@ -598,6 +663,9 @@ def main():
     cls, tot_ms = best
     launches = max(1, st["kernel_launches"][cls])
     avg_s = tot_ms / launches / 1e3
+    # work units per launch: a resident CG solve runs all its iterations in
+    # one launch (kernel_units = its CG iterations); 1 for every other class
+    units_per_launch = (st.get("kernel_units", {}).get(cls, launches) or launches) / launches
     _, nU, _ = ctx.local_size("users")
     _, nI, n_local_items = ctx.local_size("items")
     # one-pass CG on both sides at k <= 128: unsharded or with peer scalars
@@ -607,6 +675,7 @@ def main():
     onepass_of = lambda c: onepass  # noqa: E731
     nbytes, nflops = algorithmic_cost(cls, k, nU, nI, n_local_users, ldk, not args.no_fuse_start,
                                       n_local_items, onepass_of(cls))
+    nbytes, nflops = nbytes * units_per_launch, nflops * units_per_launch
     bound = "mfma" if cls.startswith("gram") and k >= 32 else "hbm"
     if bound == "hbm":
         achieved, peak, unit = nbytes / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
@@ -639,12 +708,17 @@ def main():
     for c, ms in st["kernel_ms"].items():
         n = st["kernel_launches"][c]
         if n:
+            u = st.get("kernel_units", {}).get(c, n) or n
             b, fl = algorithmic_cost(c, k, nU, nI, n_local_users, ldk, not args.no_fuse_start,
                                      n_local_items, onepass_of(c))
+            b, fl = b * u / n, fl * u / n
             kernel_table[c] = {"total_ms": round(ms, 3), "launches": n,
                                "avg_us": round(ms / n * 1e3, 2),
                                "alg_GBps": round(b / (ms / n / 1e3) / 1e9, 1) if b else None,
                                "alg_TFps": round(fl / (ms / n / 1e3) / 1e12, 2) if fl else None}
+            if u != n:
+                kernel_table[c]["cg_iterations"] = u
+                kernel_table[c]["us_per_cg_iteration"] = round(ms / u * 1e3, 2)
 
     out = {
         "metric": METRIC,
@@ -675,7 +749,8 @@ def main():
                      "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
                      "traffic": traffic,
                      "alg_bytes_per_launch": int(nbytes), "alg_flops_per_launch": int(nflops),
-                     "avg_launch_us": round(avg_s * 1e6, 2), "gather": gather},
+                     "avg_launch_us": round(avg_s * 1e6, 2), "gather": gather,
+                     "units_per_launch": round(units_per_launch, 3)},
         "iteration_roofline": iteration_roofline(k, value),
         "cg_iterations": {"users_total": st["cg_users_total"],
                           "items_total": st["cg_items_total"],
@@ -693,6 +768,9 @@ def main():
         "same_window": same_window,
         "trajectory": trajectory,
     }
+    if dist is not None:
+        out["decomposition"] = step_decomposition(st, args.steps, elapsed, ctx, k, world, dist,
+                                                  events_ms)
     if shards is not None:
         out["config"]["shards"] = shards
         out["config"]["comm"] = args.comm

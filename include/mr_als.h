@@ -49,6 +49,10 @@ enum {
   MR_K_CG_CONTROL,       /* CG scalar reduction / stop rule (both sides)      */
   MR_K_SOLVE,            /* batched Cholesky (exact mode)                      */
   MR_K_CG_START,         /* CG start of split entities (fused start)          */
+  MR_K_CG_RES_USERS,     /* resident CG solve (all iterations), user side     */
+  MR_K_CG_RES_ITEMS,     /* resident CG solve, item side                      */
+  MR_K_EXCHANGE,         /* sharded: factor all-gather of a half-step (pack,
+                            collective, unstage)                             */
   MR_K_COUNT
 };
 
@@ -61,6 +65,12 @@ typedef struct mr_stats {
   double kernel_ms[MR_K_COUNT];   /* summed HIP-event time per kernel class   */
   long long kernel_launches[MR_K_COUNT]; /* timed (non-idle) launches        */
   double phase_ms[4];             /* gram users, solve users, gram items, solve items */
+  long long kernel_units[MR_K_COUNT];   /* work units of the timed launches: CG
+                                           iterations for the resident solves,
+                                           launches for every other class   */
+  double peer_wait_ms;            /* device time the finalizing waves spent in the
+                                     peer all-reduce (sharded, peer scalars)  */
+  long long peer_reductions;      /* peer all-reduces done                    */
 } mr_stats;
 
 /* Collective callbacks for sharded runs (one process per GPU).  The engine
@@ -202,10 +212,18 @@ int mr_als_set_timing(mr_als* ctx, int enable);
  *                         320 MiB, else the default policy (a shard's side
  *                         can stay in the Infinity Cache between sweeps);
  *                         0 always default; 1 always non-temporal.  Results
- *                         are identical in every mode */
+ *                         are identical in every mode
+ *   MR_OPT_CG_RESIDENT    1 (default): a one-pass solve runs ALL its CG
+ *                         iterations in one resident launch (every block of
+ *                         the grid on the chip at once, a per-iteration
+ *                         broadcast instead of a kernel boundary; the host
+ *                         waits once per solve); 0: one launch per
+ *                         iteration.  Results are identical.  Ranks that
+ *                         share one GPU must set 0 (their resident grids
+ *                         would wait on each other): distributed.py does */
 enum { MR_OPT_FUSE_START = 0, MR_OPT_CG_SPECULATE = 1, MR_OPT_WAIT_TIMEOUT_S = 2,
        MR_OPT_CG_ONEPASS = 3, MR_OPT_GRAM_RHS_MFMA = 4, MR_OPT_CG_SWEEP = 5,
-       MR_OPT_PEER_TIMEOUT_S = 6, MR_OPT_CG_TILE_NT = 7 };
+       MR_OPT_PEER_TIMEOUT_S = 6, MR_OPT_CG_TILE_NT = 7, MR_OPT_CG_RESIDENT = 8 };
 int mr_als_set_option(mr_als* ctx, int option, double value);
 /* Ratings per Gram work item: heavier entities are split across waves and
  * their partial normal equations combined in order.  Applies to contexts
@@ -290,6 +308,9 @@ int mr_test_unstage_rows(int device, int world, int skip, const long long* rb, l
 
 const char* mr_last_error(void);
 int mr_device_count(void);
+/* PCI bus id of a visible device ("domain:bus:device.function"): tells
+ * ranks that share one physical GPU apart (MR_OPT_CG_RESIDENT). */
+int mr_device_pci_bus_id(int device, char* out, int len);
 
 #ifdef __cplusplus
 }

@@ -15,7 +15,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MR_LIB_PATH") or os.path.join(HERE, "lib", "cpp_ls_lib.so")
 
 K_NAMES = ["gram_users", "gram_items", "slab_reduce", "matvec_users",
-           "matvec_items", "cg_update", "cg_control", "solve", "cg_start_split"]
+           "matvec_items", "cg_update", "cg_control", "solve", "cg_start_split",
+           "resident_users", "resident_items", "exchange"]
 
 
 class MrStats(ctypes.Structure):
@@ -29,7 +30,10 @@ class MrStats(ctypes.Structure):
                 ("nonpd_items", ctypes.c_longlong),
                 ("kernel_ms", ctypes.c_double * len(K_NAMES)),
                 ("kernel_launches", ctypes.c_longlong * len(K_NAMES)),
-                ("phase_ms", ctypes.c_double * 4)]
+                ("phase_ms", ctypes.c_double * 4),
+                ("kernel_units", ctypes.c_longlong * len(K_NAMES)),
+                ("peer_wait_ms", ctypes.c_double),
+                ("peer_reductions", ctypes.c_longlong)]
 
     def as_dict(self):
         return {
@@ -45,6 +49,9 @@ class MrStats(ctypes.Structure):
             "kernel_launches": {n: self.kernel_launches[i] for i, n in enumerate(K_NAMES)},
             "phase_ms": {"gram_users": self.phase_ms[0], "solve_users": self.phase_ms[1],
                          "gram_items": self.phase_ms[2], "solve_items": self.phase_ms[3]},
+            "kernel_units": {n: self.kernel_units[i] for i, n in enumerate(K_NAMES)},
+            "peer_wait_ms": self.peer_wait_ms,
+            "peer_reductions": self.peer_reductions,
         }
 
 
@@ -196,6 +203,7 @@ SIGNATURES = {
     "mr_similar_last_ms": (ctypes.c_double, [VP]),
     "mr_last_error": (ctypes.c_char_p, []),
     "mr_device_count": (ctypes.c_int, []),
+    "mr_device_pci_bus_id": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
 }
 
 

@@ -292,6 +292,7 @@ int mr_als_set_option(mr_als* ctx, int option, double value) {
   switch (option) {
     case MR_OPT_FUSE_START: ctx->eng.fuse_start = value != 0.0; return 0;
     case MR_OPT_CG_ONEPASS: ctx->eng.onepass = value != 0.0; return 0;
+    case MR_OPT_CG_RESIDENT: ctx->eng.resident = value != 0.0; return 0;
     case MR_OPT_GRAM_RHS_MFMA: ctx->eng.rhs_mfma = value != 0.0; return 0;
     case MR_OPT_CG_SWEEP:
       MR_CHECK(value == 0.0 || value == 1.0 || value == 2.0, "cg_sweep must be 0, 1 or 2");
@@ -413,6 +414,8 @@ int mr_als_get_stats(mr_als* ctx, mr_stats* out) {
   MR_CHECK(ctx && out, "null argument");
   return guarded([&]() {
     if (ctx->eng.resolve_timing()) return -1;
+    if (ctx->eng.peer_account(&ctx->eng.stats.peer_wait_ms, &ctx->eng.stats.peer_reductions, false))
+      return -1;
     *out = ctx->eng.stats;
     return 0;
   });
@@ -423,7 +426,9 @@ int mr_als_reset_stats(mr_als* ctx) {
   return guarded([&]() {
     if (ctx->eng.resolve_timing()) return -1;   // drop launches timed before the reset
     ctx->eng.stats = mr_stats{};
-    return 0;
+    double w;
+    long long n;
+    return ctx->eng.peer_account(&w, &n, true);
   });
 }
 
@@ -542,6 +547,12 @@ int mr_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
   return n;
+}
+
+int mr_device_pci_bus_id(int device, char* out, int len) {
+  MR_CHECK(out && len > 0, "null argument");
+  MR_HIP(hipDeviceGetPCIBusId(out, len, device));
+  return 0;
 }
 
 }  // extern "C"

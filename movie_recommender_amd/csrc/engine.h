@@ -31,6 +31,7 @@ struct Side {
   int n_part_mv = 1;
   int n_part_op[2] = {1, 1};   // one-pass CG kernel grid (resident blocks) per tile
                                // cache policy: [0] plain loads, [1] non-temporal
+  int n_part_rs[2] = {0, 0};   // resident CG solve grid (0: not available)
   double* start_parts = nullptr;   // fused CG start: (r.r, p.Gp) per block
   int64_t n_start_pairs = 0;
 };
@@ -47,7 +48,19 @@ struct Pending {
   int cls, tag;
   hipEvent_t a, b;
   int n_real;   // CG launches with tag >= n_real ran after the solve ended
+  long long units = 1;   // work units (resident solve: its CG iterations)
 };
+
+// A resident CG solve launched but not yet read back (Engine::iterate keeps
+// up to kMaxInflight of them on the stream: the host never leaves the GPU
+// idle while it waits for a solve's published state).
+struct Inflight {
+  int seq;          // mirror sequence number of its final state
+  bool user;
+  bool started;     // fused start: iteration 0's matvec ran in the Gram
+  long long pend;   // its timing entry in `pending` (-1: not timed)
+};
+constexpr size_t kMaxInflight = 2;
 
 // One timed phase (Gram or solve of a half-step): pending entries
 // [first, last) plus, in sharded runs, a marker after the RCCL exchange.
@@ -84,6 +97,8 @@ struct Engine {
   int chunk = 2048;
   bool fuse_start = true;   // CG start in the Gram epilogue (MR_OPT_FUSE_START)
   bool onepass = true;      // one kernel per CG iteration (MR_OPT_CG_ONEPASS)
+  bool resident = true;     // one-pass solves as one resident launch (MR_OPT_CG_RESIDENT)
+  uint64_t* d_resgen = nullptr;   // the resident solve's generation words
   bool rhs_mfma = true;     // user-side rhs on the matrix cores (MR_OPT_GRAM_RHS_MFMA)
   int sweep = 1;            // one-pass sweep direction per iteration (MR_OPT_CG_SWEEP)
   int tile_nt = -1;         // one-pass G tile loads: -1 by size, 0 default policy, 1
@@ -100,6 +115,8 @@ struct Engine {
   std::vector<hipEvent_t> ev_pool;
   std::vector<Pending> pending;
   std::vector<PhaseSpan> spans;
+  std::vector<Inflight> inflight;   // deferred resident solves, oldest first
+  bool defer = false;               // half_step may leave its solve in flight
   mr_stats stats{};
   // sharded runs: native RCCL communicator (ncclComm_t) or host callbacks
   void* rccl = nullptr;
@@ -115,6 +132,8 @@ struct Engine {
   std::vector<void*> peer_opened;        // peers' buffers mapped by IPC
   bool peer_on = false;
   bool peer_used = false;                // set_peer ran (it runs once per context)
+  uint64_t peer_ticks0 = 0, peer_n0 = 0;  // PeerComm accounting at the last stats reset
+  int peer_account(double* wait_ms, long long* n, bool reset);
 
   ~Engine();
   int init(int dev, int k, int64_t U, int64_t I, int64_t n_u, const int* uv_uid,
@@ -147,19 +166,28 @@ struct Engine {
   int ag_rank() const { return rccl ? rccl_rank : comm.rank; }
   int allreduce_state_slot(int count = 1);
   int allgather_side(bool user);
+  int allgather_rows_side(bool user);
   int finalize_sharded(int phase, int seq);
   int wait_mirror(int target, CgMirror* out);
   GramDst direct_dst(Side& S);
   GramDst slab_dst(Side& S);
   int gram(Side& S, bool start = false);
   int x_ptrs(Side& S, float** xf, float** xb);
-  int cg(Side& S, double min_dec, int max_it, double* final_rr, bool started = false);
+  int cg(Side& S, double min_dec, int max_it, double* final_rr, bool started = false,
+         Inflight* deferred = nullptr);
   // the one-pass CG iteration runs this side's solve (Engine::cg)
   bool onepass_for(const Side& S) const;
-  int cg_onepass(Side& S, double min_dec, int max_it, double* final_rr, bool started);
+  // the resident launch runs this side's one-pass solve
+  bool resident_for(const Side& S) const;
+  int cg_onepass(Side& S, double min_dec, int max_it, double* final_rr, bool started,
+                 Inflight* deferred = nullptr);
   CgStart cg_start_of(Side& S);
   int solve(Side& S);
   int half_step(bool user, double min_dec, int max_it, double* final_rr);
+  // read back the deferred solves until at most `keep` remain in flight:
+  // their CG counts into the stats, errors reported here
+  int drain(size_t keep = 0);
+  void count_solve(bool user, int its, double rr);
   int run(double min_dec, int max_it);
   int iterate(int n);
   int predict(int64_t n, const int* uid, const int* iid, double* out);

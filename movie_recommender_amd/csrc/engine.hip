@@ -75,6 +75,7 @@ Engine::~Engine() {
       dfree(A->send, stream); dfree(A->recv, stream); dfree(A->rb, stream);
     }
     dfree(d_state, stream); dfree(partials, stream); dfree(d_flag, stream); dfree(xbins, stream);
+    dfree(d_resgen, stream);
     dfree(d_peer, stream);
     for (void* q : peer_opened) (void)hipIpcCloseMemHandle(q);
     if (peer_buf) (void)hipFree(peer_buf);
@@ -136,6 +137,7 @@ int Engine::toc(int cls, int tag, hipEvent_t a) {
 // Launches tagged with a CG iteration index >= their solve's n_real ran after
 // the solve had finished (early-exit no-ops) and are not counted.
 int Engine::resolve_timing() {
+  if (drain()) return -1;   // every timed resident solve knows its CG count
   if (pending.empty() && spans.empty()) return 0;
   MR_HIP(hipStreamSynchronize(stream));
   for (auto& p : pending) {
@@ -144,6 +146,7 @@ int Engine::resolve_timing() {
       MR_HIP(hipEventElapsedTime(&ms, p.a, p.b));
       stats.kernel_ms[p.cls] += ms;
       stats.kernel_launches[p.cls] += 1;
+      stats.kernel_units[p.cls] += p.units;
     }
   }
   for (auto& sp : spans) {
@@ -357,6 +360,16 @@ int Engine::build_side(Side& S, bool user, int64_t n, const int32_t* d_key,
     }
     if (parts_env > 0) op = std::min(g, parts_env);
     S.n_part_op[nt] = (int)std::max<int64_t>(1, std::min<int64_t>(op, kMaxParts));
+    // the resident solve: never more blocks than the chip holds at once
+    // (its per-iteration broadcast waits for every block)
+    S.n_part_rs[nt] = 0;
+    if (k <= kMaxK) {
+      int cus = 0;
+      MR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+      const int bpc = resident_blocks_per_cu(S.user, k, nt != 0);
+      if (bpc > 0 && cus > 0)
+        S.n_part_rs[nt] = (int)std::min<int64_t>({g, (int64_t)bpc * cus, (int64_t)kMaxParts});
+    }
   }
   MR_HIP(hipStreamSynchronize(stream));
   return 0;
@@ -386,9 +399,11 @@ int Engine::init(int dev, int k_, int64_t U_, int64_t I_, int64_t n_u,
   memset(h_mirror, 0, kMirrorSlots * sizeof(CgMirror));
   MR_HIP(hipHostGetDevicePointer((void**)&d_mirror, h_mirror, 0));
   if (dalloc(&d_state, 1, stream) || dalloc(&partials, 4 * kMaxParts, stream) ||
-      dalloc(&d_flag, 4, stream) || dalloc(&xbins, kXBinWords + kXBinStartWords, stream))
+      dalloc(&d_flag, 4, stream) || dalloc(&xbins, kXBinWords + kXBinStartWords, stream) ||
+      dalloc(&d_resgen, kResGenWords, stream))
     return -1;
   MR_HIP(hipMemsetAsync(xbins, 0, (kXBinWords + kXBinStartWords) * sizeof(int64_t), stream));
+  MR_HIP(hipMemsetAsync(d_resgen, 0, kResGenWords * sizeof(uint64_t), stream));
   // every field defined before any kernel reads it: the fused CG start
   // re-initialises the scalars but not `peer` (set only by set_peer)
   MR_HIP(hipMemsetAsync(d_state, 0, sizeof(CgState), stream));
@@ -477,6 +492,7 @@ int Engine::fac_stage(int64_t n) {
 }
 
 int Engine::set_factors(const double* hU, const double* hV) {
+  if (drain()) return -1;
   MR_HIP(hipSetDevice(device));
   const int64_t nU = U * (k + 1), nV = I * (int64_t)k;
   int rc = 0;
@@ -495,6 +511,7 @@ int Engine::set_factors(const double* hU, const double* hV) {
 }
 
 int Engine::get_factors(double* hU, double* hV) {
+  if (drain()) return -1;
   MR_HIP(hipSetDevice(device));
   const int64_t nU = U * (k + 1), nV = I * (int64_t)k;
   int rc = 0;
@@ -664,6 +681,24 @@ int Engine::peer_selftest() {
   return 0;
 }
 
+// The peer all-reduce's accounting since the last reset (stats): device
+// time of the reducing threads (s_memrealtime, 100 MHz) and reductions.
+int Engine::peer_account(double* wait_ms, long long* n, bool reset) {
+  *wait_ms = 0.0;
+  *n = 0;
+  if (!d_peer) return 0;
+  MR_HIP(hipSetDevice(device));
+  PeerComm pc{};
+  MR_D2H(&pc, d_peer, sizeof(PeerComm), stream);
+  if (reset) {
+    peer_ticks0 = pc.wait_ticks;
+    peer_n0 = pc.n_reduce;
+  }
+  *wait_ms = (double)(pc.wait_ticks - peer_ticks0) / 1e5;
+  *n = (long long)(pc.n_reduce - peer_n0);
+  return 0;
+}
+
 // Device-side latency of the peer all-reduce (collective: every rank calls it
 // with the same iters): mean microseconds per reduction over `iters`
 // back-to-back reductions by one thread, from HIP events around the kernel.
@@ -755,6 +790,21 @@ int Engine::allreduce_state_slot(int count) {
 // run the exact staging code of the RCCL path at any world size.
 int Engine::allgather_side(bool user) {
   if (!sharded()) return 0;
+  // timed as one span (MR_K_EXCHANGE): pack, the collective, unstage
+  hipEvent_t ea = nullptr, eb = nullptr;
+  if (timing) {
+    if (ev_get(&ea) || ev_get(&eb)) return -1;
+    MR_HIP(hipEventRecord(ea, stream));
+  }
+  const int rc = allgather_rows_side(user);
+  if (timing) {
+    MR_HIP(hipEventRecord(eb, stream));
+    pending.push_back({MR_K_EXCHANGE, -1, ea, eb, 1 << 30});
+  }
+  return rc;
+}
+
+int Engine::allgather_rows_side(bool user) {
   const std::vector<long long>& rb = user ? row_begin_u : row_begin_i;
   const int world = ag_world(), rank = ag_rank();
   AgStage& A = user ? ag_u : ag_i;
@@ -870,6 +920,10 @@ CgStart Engine::cg_start_of(Side& S) {
   return cs;
 }
 
+bool Engine::resident_for(const Side& S) const {
+  return resident && onepass_for(S) && S.n_part_rs[tile_nt_for(S) ? 1 : 0] > 0;
+}
+
 bool Engine::onepass_for(const Side& S) const {
   // one pass per CG iteration on both sides for k <= 128.  At k > 64 the
   // tiles stream through a register ring (tile_matvec_stream, no spills):
@@ -921,9 +975,10 @@ int Engine::x_ptrs(Side& S, float** xf, float** xb) {
 // iteration t's state is known only when the known state (after t-1) proves
 // that t cannot terminate (fails == 0, rr far above 1e-6, t+1 < max_it) --
 // so the stream stays busy without launching iterations that would be idle.
-int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr, bool started) {
+int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr, bool started,
+               Inflight* deferred) {
   if (onepass_for(S))
-    return cg_onepass(S, min_dec, max_it, final_rr, started);
+    return cg_onepass(S, min_dec, max_it, final_rr, started, deferred);
   float *xf, *xb;
   x_ptrs(S, &xf, &xb);
   const bool user = S.user;
@@ -1093,7 +1148,8 @@ int Engine::cg(Side& S, double min_dec, int max_it, double* final_rr, bool start
 // for t = 0 after a fused start); launch decisions follow exact published
 // states as in cg().  Unsharded, or sharded with the peer all-reduce (every
 // reduction happens in a last block, so ranks issue identical launches).
-int Engine::cg_onepass(Side& S, double min_dec, int max_it, double* final_rr, bool started) {
+int Engine::cg_onepass(Side& S, double min_dec, int max_it, double* final_rr, bool started,
+                       Inflight* deferred) {
   float *xf, *xb;
   x_ptrs(S, &xf, &xb);
   const bool user = S.user;
@@ -1147,8 +1203,35 @@ int Engine::cg_onepass(Side& S, double min_dec, int max_it, double* final_rr, bo
                          S.pb, S.qb, S.Cb, partials, kUpdParts, d_state, d_mirror, seq_init))
       return -1;
     if (toc(MR_K_CG_UPDATE, -1, a)) return -1;
-    if (wait_mirror(seq_init, &ms)) return -1;
+    if (!resident_for(S)) {
+      if (wait_mirror(seq_init, &ms)) return -1;
+      MR_CHECK(ms.ret >= 0, "peer all-reduce of the CG scalars timed out (a rank did not arrive)");
+    }
+  }
+  if (resident_for(S)) {
+    // every iteration and the finish in one launch (DESIGN.md "Resident CG
+    // solve"); it publishes the final state under its own sequence number
+    const bool nt = tile_nt_for(S);
+    const int seq = ++mirror_seq;
+    const int cls = user ? MR_K_CG_RES_USERS : MR_K_CG_RES_ITEMS;
+    const uint64_t tmo = (uint64_t)((peer_timeout_s + 30.0) * 1e8);   // 100 MHz ticks
+    if (tic(cls, -1, &a)) return -1;
+    if (launch_cg_resident(stream, user, d_state, started ? 1 : 0, sweep, S.E, k, S.G, S.Gs, S.Gn,
+                           S.p, S.pb, S.r, S.rb, S.q, S.qb, xf, xb, xbins, d_resgen,
+                           S.n_part_rs[nt ? 1 : 0], d_mirror, seq, nt, tmo))
+      return -1;
+    if (toc(cls, -1, a)) return -1;
+    const long long pend = timing ? (long long)pending.size() - 1 : -1;
+    if (deferred) {   // read back later (Engine::drain)
+      *deferred = Inflight{seq, user, started, pend};
+      return 0;
+    }
+    if (wait_mirror(seq, &ms)) return -1;
     MR_CHECK(ms.ret >= 0, "peer all-reduce of the CG scalars timed out (a rank did not arrive)");
+    // its CG iterations (a fused start did iteration 0's matvec itself)
+    if (pend >= 0) pending[pend].units = ms.n_matvec - (started && ms.n_matvec > 0 ? 1 : 0);
+    if (final_rr) *final_rr = ms.final_rr;
+    return ms.ret;
   }
   auto launch_iter = [&](int t) -> int {
     seq_of.push_back(++mirror_seq);
@@ -1218,6 +1301,15 @@ int Engine::solve(Side& S) {
 int Engine::half_step(bool user, double min_dec, int max_it, double* final_rr) {
   MR_HIP(hipSetDevice(device));
   Side& S = user ? su : si;
+  // a deferred solve (iterate) may only ride ahead of half-steps that
+  // report nothing: the caller of this one wants its count
+  Inflight dfr{-1, user, false, -1};
+  const bool may_defer = defer && !final_rr && solver == MR_SOLVER_CG && resident_for(S);
+  if (may_defer) {
+    if (drain(kMaxInflight - 1)) return -1;
+  } else if (drain()) {
+    return -1;
+  }
   const size_t g0 = pending.size();
   // the CG start rides on the MFMA Gram's accumulators (32 <= k <= 128)
   const bool fused = solver == MR_SOLVER_CG && fuse_start && k >= kMfmaMinK && k <= kMaxK;
@@ -1226,7 +1318,7 @@ int Engine::half_step(bool user, double min_dec, int max_it, double* final_rr) {
   int its = 0;
   double rr = 0.0;
   if (solver == MR_SOLVER_CG) {
-    its = cg(S, min_dec, max_it, &rr, fused);
+    its = cg(S, min_dec, max_it, &rr, fused, may_defer ? &dfr : nullptr);
     if (its < 0) return -1;
   } else {
     if (solve(S)) return -1;
@@ -1240,8 +1332,18 @@ int Engine::half_step(bool user, double min_dec, int max_it, double* final_rr) {
     }
     spans.push_back({user ? 0 : 2, g0, c0, nullptr});
     spans.push_back({user ? 1 : 3, c0, pending.size(), end});
-    if (pending.size() > 8192 && resolve_timing()) return -1;
   }
+  if (dfr.seq > 0) {
+    inflight.push_back(dfr);
+    return 0;
+  }
+  if (timing && pending.size() > 8192 && resolve_timing()) return -1;
+  count_solve(user, its, rr);
+  if (final_rr) *final_rr = rr;
+  return its;
+}
+
+void Engine::count_solve(bool user, int its, double rr) {
   if (user) {
     stats.last_cg_users = its;
     stats.cg_users_total += its;
@@ -1250,14 +1352,27 @@ int Engine::half_step(bool user, double min_dec, int max_it, double* final_rr) {
     stats.cg_items_total += its;
     stats.last_final_rr = rr;
   }
-  if (final_rr) *final_rr = rr;
-  return its;
+}
+
+int Engine::drain(size_t keep) {
+  while (inflight.size() > keep) {
+    const Inflight d = inflight.front();
+    inflight.erase(inflight.begin());
+    CgMirror ms{};
+    if (wait_mirror(d.seq, &ms)) return -1;
+    MR_CHECK(ms.ret >= 0, "peer all-reduce of the CG scalars timed out (a rank did not arrive)");
+    if (d.pend >= 0 && d.pend < (long long)pending.size())
+      pending[d.pend].units = ms.n_matvec - (d.started && ms.n_matvec > 0 ? 1 : 0);
+    count_solve(d.user, ms.ret, ms.final_rr);
+  }
+  return 0;
 }
 
 // The reference outer loop (matrix.cpp:810-892).  The user half-step uses
 // cg_least_squares' defaults (0.01, 200) as at :818; the item half-step passes
 // (0.01, 200, &rr) as at :854; min_r_decrease only drives the outer test.
 int Engine::run(double min_dec, int max_it) {
+  if (drain()) return -1;
   int it = 0;
   double old_rr = 0.0;
   while (it < max_it) {
@@ -1275,16 +1390,26 @@ int Engine::run(double min_dec, int max_it) {
   return it;
 }
 
+// Exactly n iterations; nothing is reported per half-step, so resident
+// solves are read back lazily (at most kMaxInflight in flight: the stream
+// always holds the next half-step while the host waits for a solve); the
+// next call that reads anything drains them.
 int Engine::iterate(int n) {
-  for (int i = 0; i < n; ++i) {
-    if (half_step(true, 0.01, 200, nullptr) < 0) return -1;
-    if (half_step(false, 0.01, 200, nullptr) < 0) return -1;
-    stats.iterations += 1;
+  defer = true;
+  int rc = 0;
+  for (int i = 0; i < n && rc == 0; ++i) {
+    if (half_step(true, 0.01, 200, nullptr) < 0 || half_step(false, 0.01, 200, nullptr) < 0)
+      rc = -1;
+    else
+      stats.iterations += 1;
   }
-  return 0;
+  defer = false;
+  if (rc) (void)drain();
+  return rc;
 }
 
 int Engine::predict(int64_t n, const int* uid, const int* iid, double* out) {
+  if (drain()) return -1;
   MR_HIP(hipSetDevice(device));
   int *du = nullptr, *di = nullptr;
   double* dout = nullptr;
@@ -1308,6 +1433,7 @@ int Engine::predict(int64_t n, const int* uid, const int* iid, double* out) {
 }
 
 int Engine::get_normal_equations(bool user, int n, const int* ents, double* G, double* c) {
+  if (drain()) return -1;
   MR_HIP(hipSetDevice(device));
   Side& S = user ? su : si;
   const int K = user ? k + 1 : k;
@@ -1373,6 +1499,7 @@ int Engine::get_layout(bool user, long long* off, int* idx, float* val, long lon
 // CG vectors r, p, q of the side as left by the last solve (K = k+1 per user
 // with the bias entry last, k per item), for tests.
 int Engine::get_cg_vectors(bool user, double* r, double* p, double* q) {
+  if (drain()) return -1;
   MR_HIP(hipSetDevice(device));
   Side& S = user ? su : si;
   const int K = user ? k + 1 : k;

@@ -2570,9 +2570,16 @@ __device__ __forceinline__ void apply_beta(CgScalars& v, double rr2) {
 // 30 s) sets `error` and the caller ends the solve with ret = -1 (the host
 // reports it) instead of spinning forever.
 // Returns false on timeout.
+__device__ __forceinline__ void peer_account(PeerComm* pc, uint64_t t0) {
+  __hip_atomic_fetch_add(&pc->wait_ticks, (uint64_t)__builtin_amdgcn_s_memrealtime() - t0,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_add(&pc->n_reduce, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ bool peer_sum(PeerComm* pc, double* vals, int count) {
-  const uint32_t s = pc->seq + 1;
-  pc->seq = s;
+  const uint64_t t_in = __builtin_amdgcn_s_memrealtime();
+  const uint32_t s = __hip_atomic_load(&pc->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  __hip_atomic_store(&pc->seq, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int world = pc->world, rank = pc->rank;
   const int64_t slot = s % kPeerSlots;
   for (int q = 0; q < world; ++q) {
@@ -2598,6 +2605,7 @@ __device__ bool peer_sum(PeerComm* pc, double* vals, int count) {
       acc[c] += __hip_atomic_load(rec + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   for (int c = 0; c < count; ++c) vals[c] = acc[c];
+  peer_account(pc, t_in);
   return true;
 }
 
@@ -2610,10 +2618,13 @@ __device__ bool peer_sum(PeerComm* pc, double* vals, int count) {
 // (every lane).
 __device__ bool peer_sum_lanes(PeerComm* pc, int64_t& val, int count) {
   const int lane = threadIdx.x & 63;
+  const uint64_t t_in = __builtin_amdgcn_s_memrealtime();
   uint32_t s = 0;
   if (lane == 0) {
-    s = pc->seq + 1;
-    pc->seq = s;
+    // sc1: the next reduction may run on another CU (the resident CG's last
+    // block changes every iteration)
+    s = __hip_atomic_load(&pc->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    __hip_atomic_store(&pc->seq, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   s = __builtin_amdgcn_readfirstlane(s);
   const int world = pc->world, rank = pc->rank;
@@ -2655,6 +2666,7 @@ __device__ bool peer_sum_lanes(PeerComm* pc, int64_t& val, int count) {
     if (lane < count) acc += __hip_atomic_load(rec + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (lane < count) val = acc;
+  if (lane == 0) peer_account(pc, t_in);
   return true;
 }
 
@@ -3015,6 +3027,177 @@ __device__ __forceinline__ void op_prof(int slot) {
   }
 }
 
+// One entity's operands of a one-pass CG iteration, loaded into registers:
+// the CG vectors' entries of this lane, the bias entries (user side) and the
+// G tiles (NB > 4: the first tiles of the stream, tile_matvec_stream loads
+// the rest).  Loading entity e + 1's while e is processed (a second register
+// set used in alternation, 2 or 3 waves / SIMD) measured 14-32 % (an 8-rank
+// shard) and 19-33 % (full size) slower per users CG iteration at k = 64
+// (profiles/r04/r04l).
+template <int NB>
+struct OpEnt {
+  static constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
+  static constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2, NTILE = NO + NF + (NB & 1);
+  static constexpr bool STREAM = MR_TS_STREAM && NB > 4;
+  static constexpr int NHELD = STREAM ? ts_ahead<NB>() : NTILE;   // tiles held per entity
+  static constexpr int64_t GS = (int64_t)NTILE * 256 + NF * 16;     // == gsize_of(k)
+  double pi[NV], ri[NV], qi[NV];
+  float xi[NV];
+  double pbias, rbias, qbias;
+  float xbias, d2;
+  float4 g[NHELD];
+};
+
+// One side's normal equations and CG vectors (local rows; x = the factor
+// table itself, warm start in place).
+struct OpSide {
+  int64_t E;
+  int k, ldk;
+  const float *G, *Gs, *Gn;
+  double *p, *pb, *r, *rb, *q, *qb;
+  float *x, *xb;
+};
+
+template <int NB, bool USER, bool NT>
+__device__ __forceinline__ void op_load(const OpSide& A, int64_t e, int update, OpEnt<NB>& E_,
+                                        int lane) {
+  using T = OpEnt<NB>;
+  const double* pe = A.p + e * A.ldk;
+  const double* re = A.r + e * A.ldk;
+  const double* qe = A.q + e * A.ldk;
+  const float* xe = A.x + e * A.ldk;
+#pragma unroll
+  for (int h = 0; h < T::NV; ++h) {
+    const int i = lane + 64 * h;
+    E_.pi[h] = (i < T::NP) ? pe[i] : 0.0;
+    E_.ri[h] = (i < T::NP) ? re[i] : 0.0;
+    E_.qi[h] = (update && i < T::NP) ? qe[i] : 0.0;
+    E_.xi[h] = (update && i < T::NP) ? xe[i] : 0.f;
+  }
+  E_.pbias = E_.rbias = E_.qbias = 0.0;
+  E_.xbias = 0.f;
+  if (USER) {
+    E_.pbias = A.pb[e];
+    E_.rbias = A.rb[e];
+    if (update) {
+      E_.qbias = A.qb[e];
+      E_.xbias = A.xb[e];
+    }
+  }
+  const floatx4* __restrict__ Ge = reinterpret_cast<const floatx4*>(A.G + e * T::GS);
+  if constexpr (T::STREAM) {
+    tile_stream_load<NB, NT>(Ge, lane, E_.g);
+  } else {
+#pragma unroll
+    for (int t = 0; t < T::NTILE; ++t) E_.g[t] = tile_ld<NT>(Ge, t, lane);
+  }
+  E_.d2 = 0.f;
+  if (T::NF > 0 && lane < 16 * T::NF) E_.d2 = A.G[e * T::GS + T::NTILE * 256 + lane];
+}
+
+// Entity e of one CG iteration (matrix.cpp:488-526 in block form): the
+// deferred x / r update of the previous iteration (update != 0), p = -r +
+// beta p, q = G p (tile GEMV) written back, and this lane's terms of p.q,
+// r.q, q.q and the updated r.r added into a, b, c, d in entity order.
+template <int NB, bool USER, bool NT>
+__device__ __forceinline__ void op_process(const OpSide& A, int64_t e, int update, double alpha,
+                                           double beta, OpEnt<NB>& E_, MvScratch<NB>& sc, double* rs,
+                                           double& a, double& b, double& c, double& d, int lane) {
+  using T = OpEnt<NB>;
+  double* pe = A.p + e * A.ldk;
+  double* re = A.r + e * A.ldk;
+  double* qe = A.q + e * A.ldk;
+  float* xe = A.x + e * A.ldk;
+  double pbias = E_.pbias, rbias = E_.rbias;
+#pragma unroll
+  for (int h = 0; h < T::NV; ++h) {
+    const int i = lane + 64 * h;
+    if (i < T::NP) {
+      double rn = E_.ri[h], pn = E_.pi[h];
+      if (update) {
+        rn = fma(alpha, E_.qi[h], E_.ri[h]);
+        re[i] = rn;
+        xe[i] = (float)fma(alpha, E_.pi[h], (double)E_.xi[h]);
+        pn = fma(beta, E_.pi[h], -rn);
+        pe[i] = pn;
+        d = fma(rn, rn, d);
+      }
+      sc.pv[virt_of(i, NB)] = pn;
+      rs[virt_of(i, NB)] = rn;
+    }
+  }
+  if (USER && update) {
+    const double rbn = fma(alpha, E_.qbias, rbias);
+    const double pbn = fma(beta, pbias, -rbn);
+    if (lane == 0) {
+      A.rb[e] = rbn;
+      A.xb[e] = (float)fma(alpha, pbias, (double)E_.xbias);
+      A.pb[e] = pbn;
+    }
+    rbias = rbn;
+    pbias = pbn;
+    if (lane == 0) d = fma(rbn, rbn, d);
+  }
+  if (T::NF > 0 && lane < 16 * T::NF) sc.dd[lane] = E_.d2;
+  __builtin_amdgcn_wave_barrier();
+  double yo[T::NV], ybv = 0.0;
+  if constexpr (T::STREAM)
+    tile_matvec_stream<NB, USER, NT>(reinterpret_cast<const floatx4*>(A.G + e * T::GS), E_.g, sc,
+                                     pbias, USER ? A.Gs + e * A.ldk : nullptr, USER ? A.Gn[e] : 0.f,
+                                     A.k, yo, ybv);
+  else
+    tile_matvec<NB, USER, (NB > 4) || MR_OP_OPAQUE>(E_.g, sc, pbias, USER ? A.Gs + e * A.ldk : nullptr,
+                                                    USER ? A.Gn[e] : 0.f, A.k, yo, ybv);
+#pragma unroll
+  for (int h = 0; h < T::NV; ++h) {
+    const int o = lane + 64 * h;
+    if (o < T::NP) {
+      const int n = nat_of(o, NB);
+      if (n < A.k) {
+        qe[n] = yo[h];
+        a = fma(yo[h], sc.pv[o], a);
+        b = fma(yo[h], rs[o], b);
+        c = fma(yo[h], yo[h], c);
+      }
+    }
+  }
+  if (USER && lane == 0) {
+    A.qb[e] = ybv;
+    a = fma(ybv, pbias, a);
+    b = fma(ybv, rbias, b);
+    c = fma(ybv, ybv, c);
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+// One chunk's four terms (lane-wise entity-order sums, reduced across the
+// wave once) into the block's order-independent containers (LDS atomics).
+__device__ __forceinline__ void op_chunk_terms(double a, double b, double c, double d,
+                                               int64_t (*xacc)[4][kXW], int lane) {
+  a = wave_sum_f64(a);
+  b = wave_sum_f64(b);
+  c = wave_sum_f64(c);
+  d = wave_sum_f64(d);
+  if (lane < kXW) {
+    atomicAdd((unsigned long long*)&xacc[0][0][lane], (unsigned long long)xterm(a, lane));
+    atomicAdd((unsigned long long*)&xacc[0][1][lane], (unsigned long long)xterm(b, lane));
+    atomicAdd((unsigned long long*)&xacc[0][2][lane], (unsigned long long)xterm(c, lane));
+    atomicAdd((unsigned long long*)&xacc[0][3][lane], (unsigned long long)xterm(d, lane));
+  }
+}
+
+// The last block's BETA step of one iteration from the collected containers
+// (lane 0's v): alpha from the direct r.r (iteration t >= 1: the residual
+// just updated, so the derivation's rounding does not accumulate across
+// iterations), r'.r' = r.r + 2 alpha r.q + alpha^2 q.q for beta and the stop.
+__device__ __forceinline__ void op_beta(CgScalars& v, const double (&sum)[4], int update) {
+  if (update) v.rr = sum[3];
+  const double al = v.rr / sum[0];
+  v.alpha = al;
+  v.n_matvec += 1;
+  apply_beta(v, fma(al * al, sum[2], fma(2.0 * al, sum[1], v.rr)));
+}
+
 template <int NB, bool USER, bool NT>
 __global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 : MR_OP_WAVES) : 2))
 #ifdef MR_OP_WPE
@@ -3030,12 +3213,8 @@ void cg_onepass_kernel(
   if (ald(&st->done)) return;
   if (threadIdx.x == 0) op_prof(8);
   const double beta = ald(&st->beta), alpha = ald(&st->alpha);
-  constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2, NTILE = NO + NF + (NB & 1);
-  constexpr int64_t GS = (int64_t)NTILE * 256 + NF * 16;   // == gsize_of(k)
-  constexpr int NP = 16 * NB, NV = (NP + 63) / 64;
   constexpr int XC = xchunk_of(NB, USER);
-  constexpr bool STREAM = MR_TS_STREAM && NB > 4;
-  constexpr int NHELD = STREAM ? ts_ahead<NB>() : NTILE;   // tiles held per entity
+  const OpSide A{E, k, ldk, G, Gs, Gn, p, pb, r, rb, q, qb, x, xb};
   __shared__ MvScratch<NB> scr[MV_WAVES];
   __shared__ double rvs[MV_WAVES][16 * NB];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -3062,133 +3241,12 @@ void cg_onepass_kernel(
     const int64_t c1 = c0 + XC < E ? c0 + XC : E;
     double a = 0.0, b = 0.0, c = 0.0;
     double d = 0.0;   // r.r of the updated residual (matrix.cpp:507's direct dot)
-    // One entity's operands: the CG vectors' entries of this lane, the bias
-    // entries (user side) and the G tiles (NB > 4: the first tiles of the
-    // stream, tile_matvec_stream loads the rest).  Loading entity e + 1's
-    // while e is processed (a second register set used in alternation, 2 or
-    // 3 waves / SIMD) measured 14-32 % (an 8-rank shard) and 19-33 % (full
-    // size) slower per users CG iteration at k = 64 (profiles/r04/r04l).
-    struct Ent {
-      double pi[NV], ri[NV], qi[NV];
-      float xi[NV];
-      double pbias, rbias, qbias;
-      float xbias, d2;
-      float4 g[NHELD];
-    };
-    auto load_ent = [&](int64_t e, Ent& E_) {
-      const double* pe = p + e * ldk;
-      const double* re = r + e * ldk;
-      const double* qe = q + e * ldk;
-      const float* xe = x + e * ldk;
-#pragma unroll
-      for (int h = 0; h < NV; ++h) {
-        const int i = lane + 64 * h;
-        E_.pi[h] = (i < NP) ? pe[i] : 0.0;
-        E_.ri[h] = (i < NP) ? re[i] : 0.0;
-        E_.qi[h] = (update && i < NP) ? qe[i] : 0.0;
-        E_.xi[h] = (update && i < NP) ? xe[i] : 0.f;
-      }
-      E_.pbias = E_.rbias = E_.qbias = 0.0;
-      E_.xbias = 0.f;
-      if (USER) {
-        E_.pbias = pb[e];
-        E_.rbias = rb[e];
-        if (update) {
-          E_.qbias = qb[e];
-          E_.xbias = xb[e];
-        }
-      }
-      const floatx4* __restrict__ Ge = reinterpret_cast<const floatx4*>(G + e * GS);
-      if constexpr (STREAM) {
-        tile_stream_load<NB, NT>(Ge, lane, E_.g);
-      } else {
-#pragma unroll
-        for (int t = 0; t < NTILE; ++t) E_.g[t] = tile_ld<NT>(Ge, t, lane);
-      }
-      E_.d2 = 0.f;
-      if (NF > 0 && lane < 16 * NF) E_.d2 = G[e * GS + NTILE * 256 + lane];
-    };
-    auto process = [&](int64_t e, Ent& E_) {
-      double* pe = p + e * ldk;
-      double* re = r + e * ldk;
-      double* qe = q + e * ldk;
-      float* xe = x + e * ldk;
-      double pbias = E_.pbias, rbias = E_.rbias;
-#pragma unroll
-      for (int h = 0; h < NV; ++h) {
-        const int i = lane + 64 * h;
-        if (i < NP) {
-          double rn = E_.ri[h], pn = E_.pi[h];
-          if (update) {
-            rn = fma(alpha, E_.qi[h], E_.ri[h]);
-            re[i] = rn;
-            xe[i] = (float)fma(alpha, E_.pi[h], (double)E_.xi[h]);
-            pn = fma(beta, E_.pi[h], -rn);
-            pe[i] = pn;
-            d = fma(rn, rn, d);
-          }
-          sc.pv[virt_of(i, NB)] = pn;
-          rs[virt_of(i, NB)] = rn;
-        }
-      }
-      if (USER && update) {
-        const double rbn = fma(alpha, E_.qbias, rbias);
-        const double pbn = fma(beta, pbias, -rbn);
-        if (lane == 0) {
-          rb[e] = rbn;
-          xb[e] = (float)fma(alpha, pbias, (double)E_.xbias);
-          pb[e] = pbn;
-        }
-        rbias = rbn;
-        pbias = pbn;
-        if (lane == 0) d = fma(rbn, rbn, d);
-      }
-      if (NF > 0 && lane < 16 * NF) sc.dd[lane] = E_.d2;
-      __builtin_amdgcn_wave_barrier();
-      double yo[NV], ybv = 0.0;
-      if constexpr (STREAM)
-        tile_matvec_stream<NB, USER, NT>(reinterpret_cast<const floatx4*>(G + e * GS), E_.g, sc,
-                                         pbias, USER ? Gs + e * ldk : nullptr, USER ? Gn[e] : 0.f,
-                                         k, yo, ybv);
-      else
-        tile_matvec<NB, USER, (NB > 4) || MR_OP_OPAQUE>(E_.g, sc, pbias, USER ? Gs + e * ldk : nullptr,
-                                                        USER ? Gn[e] : 0.f, k, yo, ybv);
-#pragma unroll
-      for (int h = 0; h < NV; ++h) {
-        const int o = lane + 64 * h;
-        if (o < NP) {
-          const int n = nat_of(o, NB);
-          if (n < k) {
-            qe[n] = yo[h];
-            a = fma(yo[h], sc.pv[o], a);
-            b = fma(yo[h], rs[o], b);
-            c = fma(yo[h], yo[h], c);
-          }
-        }
-      }
-      if (USER && lane == 0) {
-        qb[e] = ybv;
-        a = fma(ybv, pbias, a);
-        b = fma(ybv, rbias, b);
-        c = fma(ybv, ybv, c);
-      }
-      __builtin_amdgcn_wave_barrier();
-    };
     for (int64_t e = c0; e < c1; ++e) {
-      Ent cur;
-      load_ent(e, cur);
-      process(e, cur);
+      OpEnt<NB> cur;
+      op_load<NB, USER, NT>(A, e, update, cur, lane);
+      op_process<NB, USER, NT>(A, e, update, alpha, beta, cur, sc, rs, a, b, c, d, lane);
     }
-    a = wave_sum_f64(a);
-    b = wave_sum_f64(b);
-    c = wave_sum_f64(c);
-    d = wave_sum_f64(d);
-    if (lane < kXW) {
-      atomicAdd((unsigned long long*)&xacc[0][0][lane], (unsigned long long)xterm(a, lane));
-      atomicAdd((unsigned long long*)&xacc[0][1][lane], (unsigned long long)xterm(b, lane));
-      atomicAdd((unsigned long long*)&xacc[0][2][lane], (unsigned long long)xterm(c, lane));
-      atomicAdd((unsigned long long*)&xacc[0][3][lane], (unsigned long long)xterm(d, lane));
-    }
+    op_chunk_terms(a, b, c, d, xacc, lane);
   }
   if (threadIdx.x == 0) op_prof(9);
   xsum_flush_lds<4>(xacc, xbins, 1);
@@ -3229,20 +3287,253 @@ void cg_onepass_kernel(
     double sum[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) sum[j] = xv[j];
-    // iteration t >= 1: alpha and the next r'.r' start from the DIRECT r.r of
-    // the residual just updated, not from the previous kernel's derived value,
-    // so the derivation's rounding does not accumulate across iterations
-    // (the derived value set only the previous beta and stop test)
-    if (update) v.rr = sum[3];
-    const double al = v.rr / sum[0];
-    v.alpha = al;
-    v.n_matvec += 1;
-    apply_beta(v, fma(al * al, sum[2], fma(2.0 * al, sum[1], v.rr)));
+    op_beta(v, sum, update);
     store_state(st, v);
     ast(&st->pending, 1);
     op_prof(2);
     publish(v, mirror, seq);
     op_prof(3);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Resident CG solve (DESIGN.md "Resident CG solve"): the one-pass iteration
+// above for EVERY iteration of a solve in ONE launch.  The grid is exactly
+// the blocks the chip holds at once, so all blocks are resident; each wave
+// OWNS a fixed set of entity chunks for the whole solve (the one-pass deal of
+// chunk j to wave j mod (4 x grid), its order reversed on alternate
+// iterations instead of the deal), so the CG vectors of an entity are only
+// ever touched by one wave: no cross-CU hand-off of the vectors, no kernel
+// boundary (launch ramp, dirty-L2 write-back) between iterations.  Per
+// iteration, as one pass: chunks -> containers -> bins; arrival; the last
+// block takes alpha, r'.r' and the BETA rule (and the peer all-reduce) and
+// broadcasts {alpha, beta, done} to every block through a generation word
+// (write-through sc1 stores, drained, then the word: MI355X_MICROARCH.md
+// "Valid forms", first table row); the others poll it.  While they wait, each
+// wave already loads its first entity of the next iteration (G tiles and its
+// own vectors).  After the stop the pending x update (the UPD_FINISH pass)
+// is applied by every wave to its own entities.  The arithmetic is the
+// one-pass kernel's, term for term: every chunk's terms and every vector
+// entry are bitwise those of the launch-per-iteration path.
+// The state a block reads after the broadcast was written by another
+// block (another XCD): in this kernel the state goes through sc1 loads and
+// stores only.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ CgScalars load_state_sc1(CgState* st) {
+  CgScalars v;
+  auto ld = [](auto* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  v.rr = ld(&st->rr);
+  v.alpha = ld(&st->alpha);
+  v.beta = ld(&st->beta);
+  v.final_rr = ld(&st->final_rr);
+  v.min_dec = ld(&st->min_dec);
+  v.comm0 = ld(&st->comm[0]);
+  v.comm1 = ld(&st->comm[1]);
+  v.it = ld(&st->it);
+  v.fails = ld(&st->fails);
+  v.done = ld(&st->done);
+  v.ret = ld(&st->ret);
+  v.max_it = ld(&st->max_it);
+  v.n_matvec = ld(&st->n_matvec);
+  v.sharded = ld(&st->sharded);
+  return v;
+}
+__device__ __forceinline__ void store_state_sc1(CgState* st, const CgScalars& v) {
+  auto s = [](auto* p, auto x) { __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  s(&st->rr, v.rr);
+  s(&st->alpha, v.alpha);
+  s(&st->beta, v.beta);
+  s(&st->final_rr, v.final_rr);
+  s(&st->min_dec, v.min_dec);
+  s(&st->comm[0], v.comm0);
+  s(&st->comm[1], v.comm1);
+  s(&st->it, v.it);
+  s(&st->fails, v.fails);
+  s(&st->done, v.done);
+  s(&st->ret, v.ret);
+  s(&st->max_it, v.max_it);
+  s(&st->n_matvec, v.n_matvec);
+  s(&st->sharded, v.sharded);
+}
+
+// MR_RS_PREFETCH 1: each wave loads its first entity of iteration t + 1
+// while it waits for iteration t's broadcast (holds the operands across the
+// barrier)
+#ifndef MR_RS_PREFETCH
+#define MR_RS_PREFETCH 0
+#endif
+template <int NB, bool USER, bool NT>
+__global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 : MR_OP_WAVES) : 2))
+void cg_resident_kernel(CgState* __restrict__ st, int t0, int sweep, OpSide A,
+                        int64_t* __restrict__ xbins, uint64_t* __restrict__ gen,
+                        CgMirror* mirror, int seq, uint64_t tmo) {
+  constexpr int XC = xchunk_of(NB, USER);
+  using T = OpEnt<NB>;
+  __shared__ MvScratch<NB> scr[MV_WAVES];
+  __shared__ double rvs[MV_WAVES][16 * NB];
+  __shared__ int64_t xacc[1][4][kXW];
+  __shared__ double s_ab[2];
+  __shared__ int s_flag[2];   // [0]: broadcast done (2: failed), [1]: last block
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wu = __builtin_amdgcn_readfirstlane(wid);
+  const int64_t nch = (A.E + XC - 1) / XC;
+  const int64_t j0 = (int64_t)blockIdx.x * MV_WAVES + wu, js = (int64_t)gridDim.x * MV_WAVES;
+  const int64_t cnt = j0 < nch ? (nch - 1 - j0) / js + 1 : 0;   // chunks this wave owns
+  // the i-th chunk of a sweep: ascending, or descending on reversed sweeps
+  // (MR_OPT_CG_SWEEP: 1 = iteration 1 backwards, then alternate)
+  auto rev_of = [&](int t) { return sweep == 0 ? 0 : ((t & 1) ^ (sweep == 2 ? 1 : 0)); };
+  auto chunk0 = [&](int64_t i, int rev) { return (j0 + (rev ? cnt - 1 - i : i) * js) * XC; };
+  // the state at entry was written by the previous kernels of the stream
+  double alpha = ald(&st->alpha), beta = ald(&st->beta);
+  int done = ald(&st->done);
+  if (threadIdx.x < 4 * kXW) (&xacc[0][0][0])[threadIdx.x] = 0;
+  if (done) {
+    // ended at the start: publish for the host; the start's pending update
+    if (blockIdx.x == 0 && threadIdx.x == 0) publish(load_state(st), mirror, seq);
+    if (!ald(&st->pending)) return;
+  }
+  int t = t0;
+  OpEnt<NB> cur;
+  if (MR_RS_PREFETCH && !done && cnt > 0) op_load<NB, USER, NT>(A, chunk0(0, rev_of(t)), t > 0, cur, lane);
+  __syncthreads();
+  while (!done) {
+    const int update = t > 0, rev = rev_of(t);
+    const int lo = lane;
+    MvScratch<NB>& sci = scr[wid];
+    double* rsi = rvs[wid];
+    for (int64_t i = 0; i < cnt; ++i) {
+      const int64_t c0 = chunk0(i, rev);
+      const int64_t c1 = c0 + XC < A.E ? c0 + XC : A.E;
+      double a = 0.0, b = 0.0, c = 0.0, d = 0.0;
+      for (int64_t e = c0; e < c1; ++e) {
+        if (!MR_RS_PREFETCH || i != 0 || e != c0) op_load<NB, USER, NT>(A, e, update, cur, lo);
+        op_process<NB, USER, NT>(A, e, update, alpha, beta, cur, sci, rsi, a, b, c, d, lo);
+      }
+      op_chunk_terms(a, b, c, d, xacc, lo);
+    }
+    // the block's containers into the bins (and cleared for the next
+    // iteration by the thread that read them), then the arrival.  Every
+    // thread-derived address below comes from a fresh opaque copy of the
+    // thread index: hoisted out of the iteration loop, these addresses would
+    // stay live across the GEMV (17 VGPRs spilled at NB = 4)
+    __syncthreads();
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    if (tid < 4 * kXW) {
+      const int v = tid / kXW, dd = tid % kXW;
+      const int64_t tt = xacc[0][v][dd];
+      xacc[0][v][dd] = 0;
+      if (tt != 0)
+        __hip_atomic_fetch_add(xbins + ((int64_t)(blockIdx.x % kXBins) * 4 + v) * kXW + dd, tt,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (threadIdx.x == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      s_flag[1] = __hip_atomic_fetch_add(&st->arrive, 1u, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    }
+    __syncthreads();
+    const bool fin = s_flag[1] && wid == 0;
+    const uint64_t want = ((uint64_t)(uint32_t)seq << 32) | (uint32_t)(t + 1);
+    // this wave's own stores of the iteration are complete before it
+    // re-reads its first entity's vectors for the next one
+    if (MR_RS_PREFETCH) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (!fin && cnt > 0) op_load<NB, USER, NT>(A, chunk0(0, rev_of(t + 1)), 1, cur, lane);
+    }
+    if (fin) {
+      __shared__ int64_t xs[4 * kXW];
+      __shared__ double xv[4];
+      const int lane = tid & 63;
+      PeerComm* pc = ald(&st->peer);
+      CgScalars v{};
+      if (lane == 0) v = load_state_sc1(st);
+      int64_t tot = xsum_collect<4>(xbins, lane);
+      if (lane == 0) __hip_atomic_store(&st->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int flag = 0;
+      if (pc && !peer_sum_lanes(pc, tot, 4 * kXW)) {
+        if (lane == 0) {
+          v.done = 1;
+          v.ret = -1;
+          store_state_sc1(st, v);
+          publish(v, mirror, seq);
+        }
+        flag = 2;
+      } else {
+        if (lane < 4 * kXW) xs[lane] = tot;
+        __builtin_amdgcn_wave_barrier();
+        if (lane < 4) xv[lane] = xsum_value(&xs[lane * kXW]);
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {
+          double sum[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) sum[j] = xv[j];
+          op_beta(v, sum, update);
+          store_state_sc1(st, v);
+          __hip_atomic_store(&st->pending, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (v.done) publish(v, mirror, seq);
+          flag = v.done;
+        }
+      }
+      if (lane == 0) {
+        __hip_atomic_store(&st->res_alpha, v.alpha, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&st->res_beta, v.beta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&st->res_done, flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      // every store above (state, broadcast, the bins' clears) written
+      // through and drained before the generation word moves
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane < kResGenCopies)
+        __hip_atomic_store(gen + lane * kResGenStride, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (MR_RS_PREFETCH && cnt > 0) op_load<NB, USER, NT>(A, chunk0(0, rev_of(t + 1)), 1, cur, lane);
+    }
+    if (threadIdx.x == 0) {
+      const uint64_t* g = gen + (blockIdx.x % kResGenCopies) * kResGenStride;
+      const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+      int ok = 1;
+      while (__hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
+        if (__builtin_amdgcn_s_memrealtime() - t_start > tmo) {
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      s_ab[0] = __hip_atomic_load(&st->res_alpha, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_ab[1] = __hip_atomic_load(&st->res_beta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_flag[0] = ok ? __hip_atomic_load(&st->res_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 2;
+    }
+    __syncthreads();
+    // wave-uniform values back into scalar registers (LDS loads land in VGPRs)
+    alpha = __builtin_bit_cast(double, ((int64_t)__builtin_amdgcn_readfirstlane(
+                                           (int)__builtin_bit_cast(int64_t, s_ab[0])) & 0xFFFFFFFFll) |
+                                       (int64_t)__builtin_amdgcn_readfirstlane(
+                                           (int)(__builtin_bit_cast(int64_t, s_ab[0]) >> 32)) << 32);
+    beta = __builtin_bit_cast(double, ((int64_t)__builtin_amdgcn_readfirstlane(
+                                          (int)__builtin_bit_cast(int64_t, s_ab[1])) & 0xFFFFFFFFll) |
+                                      (int64_t)__builtin_amdgcn_readfirstlane(
+                                          (int)(__builtin_bit_cast(int64_t, s_ab[1]) >> 32)) << 32);
+    done = __builtin_amdgcn_readfirstlane(s_flag[0]);
+    if (done == 2) return;   // failed peer exchange or a broadcast that never came
+    ++t;
+    __syncthreads();   // s_ab / s_flag are rewritten by the next iteration
+  }
+  // the stopped iteration's x update (UPD_FINISH), entry by entry on this
+  // wave's own entities: x += alpha p (its residual update would be dead)
+  for (int64_t i = 0; i < cnt; ++i) {
+    const int64_t c0 = chunk0(i, 0);
+    const int64_t c1 = c0 + XC < A.E ? c0 + XC : A.E;
+    for (int64_t e = c0; e < c1; ++e) {
+#pragma unroll
+      for (int h = 0; h < T::NV; ++h) {
+        const int ii = lane + 64 * h;
+        if (ii < T::NP) {
+          float* xe = A.x + e * A.ldk + ii;
+          *xe = (float)fma(alpha, A.p[e * A.ldk + ii], (double)*xe);
+        }
+      }
+      if (USER && lane == 0) A.xb[e] = (float)fma(alpha, A.pb[e], (double)A.xb[e]);
+    }
   }
 }
 
@@ -3297,6 +3588,55 @@ int launch_cg_onepass(hipStream_t s, bool user_side, CgState* st, int update, in
   }
 #undef MR_OP_CASE
 #undef MR_OP_LAUNCH
+  MR_HIP(hipGetLastError());
+  return 0;
+}
+
+int resident_blocks_per_cu(bool user_side, int k, bool nt) {
+  const void* f = nullptr;
+#define MR_RS_FN(NB)                                                                        \
+  case NB:                                                                                  \
+    if (nt) f = user_side ? (const void*)cg_resident_kernel<NB, true, true>                 \
+                          : (const void*)cg_resident_kernel<NB, false, true>;               \
+    else f = user_side ? (const void*)cg_resident_kernel<NB, true, false>                   \
+                       : (const void*)cg_resident_kernel<NB, false, false>;                 \
+    break;
+  switch (nb16_of(k)) {
+    MR_RS_FN(1) MR_RS_FN(2) MR_RS_FN(3) MR_RS_FN(4)
+    MR_RS_FN(5) MR_RS_FN(6) MR_RS_FN(7) MR_RS_FN(8)
+    default: return 0;
+  }
+#undef MR_RS_FN
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, 256, 0) != hipSuccess) return 0;
+  return n;
+}
+
+int launch_cg_resident(hipStream_t s, bool user_side, CgState* st, int t0, int sweep, int64_t E,
+                       int k, const float* G, const float* Gs, const float* Gn, double* p,
+                       double* pb, double* r, double* rb, double* q, double* qb, float* x,
+                       float* xb, int64_t* xbins, uint64_t* gen, int n_part, CgMirror* mirror,
+                       int seq, bool nt, uint64_t timeout_ticks) {
+  if (n_part <= 0) return 0;
+  const OpSide A{E, k, ldk_of(k), G, Gs, Gn, p, pb, r, rb, q, qb, x, xb};
+#define MR_RS_LAUNCH(NB, U, T)                                                              \
+  MR_LAUNCH((cg_resident_kernel<NB, U, T>), dim3(n_part), dim3(256), 0, s, st, t0, sweep, A,   \
+            xbins, gen, mirror, seq, timeout_ticks)
+#define MR_RS_CASE(NB)                                                                      \
+  case NB:                                                                                  \
+    if (user_side) {                                                                        \
+      if (nt) MR_RS_LAUNCH(NB, true, true); else MR_RS_LAUNCH(NB, true, false);             \
+    } else {                                                                                \
+      if (nt) MR_RS_LAUNCH(NB, false, true); else MR_RS_LAUNCH(NB, false, false);           \
+    }                                                                                       \
+    break;
+  switch (nb16_of(k)) {
+    MR_RS_CASE(1) MR_RS_CASE(2) MR_RS_CASE(3) MR_RS_CASE(4)
+    MR_RS_CASE(5) MR_RS_CASE(6) MR_RS_CASE(7) MR_RS_CASE(8)
+    default: set_error("resident CG needs k <= 128"); return -1;
+  }
+#undef MR_RS_CASE
+#undef MR_RS_LAUNCH
   MR_HIP(hipGetLastError());
   return 0;
 }

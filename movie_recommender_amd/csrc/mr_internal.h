@@ -193,6 +193,9 @@ struct PeerComm {
   uint64_t timeout_ticks;  // give up on a peer after this many s_memrealtime
                            // ticks (100 MHz; MR_OPT_PEER_TIMEOUT_S)
   double* buf[kMaxPeers];  // rank q's exchange buffer, mapped into this process
+  // accounting (mr_stats peer_wait_ms / peer_reductions): s_memrealtime
+  // ticks the reducing thread spent inside reductions, and their number
+  uint64_t wait_ticks, n_reduce;
 };
 
 // One peer reduction of {rank + 1, 1} into out[0..2] = {sum, count, ok}.
@@ -226,7 +229,18 @@ struct CgState {
                     // "One-pass CG iteration"); set by the host per solve
   int32_t pending;  // one-pass: the last iteration's x / r update is not applied yet
   uint32_t arrive_start;  // cg_start_split blocks finished (folded CG_START control)
+  // resident CG solve (cg_resident_kernel): the last block's per-iteration
+  // broadcast to every block, written and read with sc1 (write-through)
+  // accesses; res_done 1: stopped, 2: failed
+  double res_alpha, res_beta;
+  int32_t res_done;
 };
+// Generation words of the resident CG's per-iteration broadcast: 16 copies
+// on lines of their own (block b polls copy b mod 16), each bumped by the
+// last block to (seq << 32) | (t + 1) after iteration t.
+constexpr int kResGenCopies = 16;
+constexpr int kResGenStride = 16;   // uint64 words: 128 B per copy
+constexpr int kResGenWords = kResGenCopies * kResGenStride;
 // The CG_START control folded into cg_start_split's last block (one-pass
 // solves with split entities): st == nullptr keeps the separate control launch.
 struct CgMirror;
@@ -244,7 +258,7 @@ struct StartFold {
 // state under a sequence number into slot seq % kMirrorSlots (seqlock: odd
 // while being written), so the host reads the state of an EXACT iteration --
 // what makes launch decisions identical on every rank of a sharded run.
-constexpr int kMirrorSlots = 8;
+constexpr int kMirrorSlots = 32;
 struct CgMirror {
   int32_t seq;
   int32_t done;
@@ -314,6 +328,20 @@ int launch_cg_onepass(hipStream_t s, bool user_side, CgState* st, int update, in
                       const float* G, const float* Gs, const float* Gn, double* p, double* pb,
                       double* r, double* rb, double* q, double* qb, float* x, float* xb,
                       int64_t* xbins, int n_part, CgMirror* mirror, int seq, bool nt);
+// Resident CG solve (kernels.hip cg_resident_kernel): every iteration of
+// one solve in one launch, from iteration t0 (0: unfused start, 1: after a
+// fused start) until the stop; publishes the final state under `seq` and
+// applies the pending x update.  Needs every block of the grid resident at
+// once: n_part = resident_blocks_per_cu(...) x CUs at most.  gen:
+// kResGenWords uint64 (any content except a value (seq << 32) | t of this
+// launch).  timeout_ticks (100 MHz): a block whose broadcast does not come
+// gives up (the host's wait then reports the unpublished state).
+int resident_blocks_per_cu(bool user_side, int k, bool nt);
+int launch_cg_resident(hipStream_t s, bool user_side, CgState* st, int t0, int sweep, int64_t E,
+                       int k, const float* G, const float* Gs, const float* Gn, double* p,
+                       double* pb, double* r, double* rb, double* q, double* qb, float* x,
+                       float* xb, int64_t* xbins, uint64_t* gen, int n_part, CgMirror* mirror,
+                       int seq, bool nt, uint64_t timeout_ticks);
 // x is the fp32 factor table (and bias), r / p / q the fp64 CG vectors;
 // nt: non-temporal G tile loads (Engine::tile_nt_for);
 // xbins: kXBins x 4 x 11 int64 bins of the order-independent sums (zero

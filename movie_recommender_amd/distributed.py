@@ -232,7 +232,25 @@ def attach_peer_scalars(ctx, rank, world, _fail_set_peer=False):
     if not agree(L.mr_als_peer_selftest(ctx._h) == 0):
         return reset()
     ctx._peer = joined
+    if ranks_share_a_gpu(ctx):
+        # two resident CG grids on one GPU would each hold every CU slot
+        # while waiting for the other's reduction (include/mr_als.h
+        # MR_OPT_CG_RESIDENT): one launch per CG iteration instead
+        ctx.set_option("cg_resident", 0)
     return True
+
+
+def ranks_share_a_gpu(ctx):
+    """Collective: True when two ranks of the group run on one physical GPU
+    (same host and PCI bus id) -- the test layouts with --device-map 0,0."""
+    import socket
+    import torch.distributed as dist
+    buf = ctypes.create_string_buffer(64)
+    _lib.check(_lib.lib().mr_device_pci_bus_id(ctx.device, buf, 64), "mr_device_pci_bus_id")
+    me = (socket.gethostname(), buf.value.decode())
+    allr = [None] * dist.get_world_size()
+    dist.all_gather_object(allr, me)
+    return len(set(allr)) < len(allr)
 
 
 def sharded_context(user_ids, item_ids, ratings, k, num_users, num_items, device,

@@ -14,7 +14,7 @@ from . import _lib
 SOLVERS = {"cg": 0, "cholesky": 1}
 OPTIONS = {"fuse_start": 0, "cg_speculate": 1, "wait_timeout_s": 2,
            "cg_onepass": 3, "gram_rhs_mfma": 4, "cg_sweep": 5,
-           "peer_timeout_s": 6, "cg_tile_nt": 7}   # include/mr_als.h
+           "peer_timeout_s": 6, "cg_tile_nt": 7, "cg_resident": 8}   # include/mr_als.h
 
 
 def _i32(a):
@@ -38,6 +38,7 @@ class AlsContext:
                  device=0, solver="cg", ridge=0.0, timing=False,
                  user_range=None, item_range=None, item_view=None, gram_chunk=None):
         L = _lib.lib()
+        self.device = int(device)
         self.k = int(k)
         self.num_users = int(num_users)
         self.num_items = int(num_items)

@@ -63,3 +63,15 @@ def test_bench_gpus2_matches_gpus1(gpu):
     assert a["trajectory"]["matches_timed_region"] and b["trajectory"]["matches_timed_region"]
     assert a["same_window"]["cg_users"] == b["same_window"]["cg_users"]
     assert a["same_window"]["trajectory_cg_matches"]
+    # the sharded line decomposes its step (VERDICT r05 "do this" 3)
+    dc = b["decomposition"]
+    assert dc["exchange_ms_per_step"] > 0 and dc["peer_wait_ms_per_step"] > 0
+    assert dc["peer_reductions_per_step"] >= 2     # >= one per half-step's solve
+    assert len(dc["compute_ms_per_step_by_rank"]) == 2
+    assert min(dc["compute_ms_per_step_by_rank"]) > 0
+    assert dc["step_ms_max"] >= dc["step_ms_min"] > 0
+    assert abs(dc["step_ms_max"] - b["ms_per_step"]) <= 1e-3 * b["ms_per_step"] + 1e-3
+    m = dc["model"]
+    assert dc["model_step_ms"] == pytest.approx(m["compute_ms"] + m["exchange_ms"]
+                                                + m["peer_reductions_ms"], abs=1e-3)
+    assert "decomposition" not in a

@@ -263,6 +263,52 @@ def test_cg_sweep_direction_is_bitwise_neutral(gpu, k):
         assert np.array_equal(U, U1) and np.array_equal(V, V1)
 
 
+@pytest.mark.parametrize("k,fuse,chunk,scale", [(64, 1, 2048, 0.02), (64, 0, 2048, 0.02),
+                                               (64, 1, 64, 0.02), (32, 1, 2048, 0.02),
+                                               (10, 1, 2048, 0.02), (96, 1, 2048, 0.02),
+                                               (120, 1, 64, 0.05), (128, 1, 2048, 0.2)])
+def test_resident_solve_bitwise_equals_launch_per_iteration(gpu, k, fuse, chunk, scale):
+    """MR_OPT_CG_RESIDENT (one launch per solve, every block resident, a
+    per-iteration broadcast) against one launch per CG iteration: the same
+    arithmetic term for term, so ret, the CG counts, the final rr and the
+    factors are bitwise identical -- fused and unfused starts, split
+    entities (chunk 64), NB = 1 ... 8 (k = 10 ... 128), every sweep mode, and
+    max_iteration limits that stop a solve at its start or mid-way."""
+    from movie_recommender_amd import synth
+    from movie_recommender_amd.engine import AlsContext
+    from movie_recommender_amd import _lib
+    rs = synth.movielens_like("ml-full", k, scale=scale)
+    rng = np.random.RandomState(3)
+    U0 = rng.uniform(-1, 1, rs.num_users * (k + 1))
+    V0 = rng.uniform(-1, 1, rs.num_items * k)
+    try:
+        with AlsContext(rs.user_ids, rs.item_ids, rs.ratings, k, rs.num_users, rs.num_items,
+                        gram_chunk=chunk) as ctx:
+            ctx.set_option("fuse_start", fuse)
+            ctx.set_timing(True)
+            for sweep in ((1,) if k != 64 or chunk != 2048 else (0, 1, 2)):
+                ctx.set_option("cg_sweep", sweep)
+                outs = []
+                for resident in (0, 1):
+                    ctx.set_option("cg_resident", resident)
+                    ctx.set_factors(U0, V0)
+                    ctx.reset_stats()
+                    ctx.iterate(2)
+                    trace = [ctx.half_step(side, 0.01, m) for side, m in
+                             (("users", 0), ("items", 1), ("users", 3), ("items", 200))]
+                    st = ctx.stats()
+                    outs.append((ctx.get_factors(), st["cg_users_total"], st["cg_items_total"],
+                                 trace, st["kernel_launches"]["resident_users"]))
+                (Ua, Va), cua, cia, tra, nra = outs[0]
+                (Ub, Vb), cub, cib, trb, nrb = outs[1]
+                assert nra == 0 and nrb > 0, (nra, nrb)
+                assert (cua, cia) == (cub, cib) and cua + cia > 4, (cua, cia, cub, cib)
+                assert tra == trb, (tra, trb)
+                assert np.array_equal(Ua, Ub) and np.array_equal(Va, Vb)
+    finally:
+        _lib.check(_lib.lib().mr_set_gram_chunk(2048), "reset chunk")
+
+
 @pytest.mark.parametrize("ratings", ["normal", "halfstar"])
 @pytest.mark.parametrize("k", [3, 10, 16, 20, 32, 33, 64, 65, 96, 120, 128, 144, 200, 300])
 def test_gram_kernel_vs_numpy(gpu, k, ratings):
@@ -546,78 +592,66 @@ def _gpu_rank_agreement(rs, U, V, k):
     return float(np.nanmean(a)), int(np.count_nonzero(~np.isnan(a)))
 
 
-def test_band_headline_shape_heldout_rmse(gpu):
-    """G4 at the headline shape (round 3): MovieLens-full-shaped synthetic
-    data, k = 64, 20 % of each user's ratings held out, the reference's loop
-    with max_iteration 4, initial factors from seeds 0..4 -- against the
-    compiled reference's runs of the same 5 seeds at several thread counts
-    (band_mlfull_k64.json from tests/golden/make_golden.py g9).  The
-    reference is chaotic here (one seed's held-out RMSE moves 0.954 .. 1.007
-    between its own thread counts), so the GPU is one more "thread count" of
-    each seed: per seed, its held-out RMSE and its mean ranking agreement (the
-    reference's own quality metric, my_util.py:101-145, computed on the GPU)
-    must lie within that seed's reference range widened by W, the largest
-    range the reference itself shows between thread counts at any one seed
-    (its run-to-run chaos), and the 5-seed means within the pooled range.  The
-    GPU values are reported in a warning (kept in the pytest summary)."""
+def test_distribution_headline_config(gpu):
+    """Realistic-data parity at the headline config (VERDICT r05 "do this"
+    2; BASELINE.json metric "... RMSE parity"): the MovieLens-full-shaped
+    synthetic set at k = 64 with 20 % of each user's ratings held out.  The
+    compiled reference ran 20 initial-factor seeds x thread counts {1, 2, 4}
+    with its OWN outer stop (max_iteration 200, matrix.cpp:871-875;
+    dist_mlfull_k64.json from tests/golden/make_golden.py g13); the GPU runs
+    the same 20 seeds once each through the product path.  The reference is
+    chaotic here (one seed's held-out RMSE moves by up to ~0.05 between its
+    own thread counts), so parity is a two-sample statement on held-out
+    RMSE, train RMSE, ``ret`` and the reference's own quality metric (mean
+    per-user rank agreement, my_util.py:101-145, computed by the GPU
+    evaluation path): dist_stats.failing -- the two-sided Mann-Whitney of the
+    20 GPU runs against the 60 reference runs at p >= 0.05 per metric, and
+    the seed-stratified permutation test with Holm's correction (family-wise
+    0.05).  Sanity bound beside it: each seed's GPU RMSE inside that seed's
+    reference range widened by W, the largest range at any seed."""
     import warnings
+    import dist_stats as DS
     from movie_recommender_amd import synth
     from movie_recommender_amd.engine import AlsContext
     from oracle import als_oracle as O
     from oracle.ref import init_factors
-    with open(os.path.join(GOLDEN, "band_mlfull_k64.json")) as f:
-        band = json.load(f)
-    k, mi = band["k"], band["max_iteration"]
-    rs = synth.movielens_like(band["shape"], k, seed=band["data_seed"],
-                              test_ratio=band["test_ratio"])
-    assert rs.n == band["n_train"] and abs(float(np.sum(rs.ratings)) - band["ratings_checksum"]) < 1e-6
-    assert len(band["runs"]) >= 15
-    pool = {m: (min(r[m] for r in band["runs"]), max(r[m] for r in band["runs"]))
-            for m in ("test_rmse", "rank_agreement")}
-    seeds = sorted({r["seed"] for r in band["runs"]})
-    chaos = {m: max(max(r[m] for r in band["runs"] if r["seed"] == sd)
-                    - min(r[m] for r in band["runs"] if r["seed"] == sd) for sd in seeds)
-             for m in pool}
-    got = {"test_rmse": [], "rank_agreement": [], "train_rmse": [], "ret": []}
-    report = []
-    for seed in seeds:
+    path = os.path.join(GOLDEN, "dist_mlfull_k64.json")
+    if not os.path.exists(path):
+        pytest.skip("dist_mlfull_k64.json not generated (make_golden.py g13)")
+    with open(path) as f:
+        dist = json.load(f)
+    k = dist["k"]
+    rs = synth.movielens_like(dist["shape"], k, seed=dist["data_seed"],
+                              test_ratio=dist["test_ratio"])
+    assert rs.n == dist["n_train"] and len(rs.test_ratings) == dist["n_test"]
+    assert abs(float(np.sum(rs.ratings)) - dist["ratings_checksum"]) < 1e-6
+    pool = DS.runs_of(dist, "ref")
+    assert len(pool) >= 20 * 3 and dist["max_iteration"] == 200
+    got = []
+    for seed in range(dist["n_seeds"]):
         U0, V0 = init_factors(rs.num_users, rs.num_items, k, seed)
         with AlsContext(rs.user_ids, rs.item_ids, rs.ratings, k, rs.num_users,
                         rs.num_items) as ctx:
             ctx.set_factors(U0, V0)
-            ret = ctx.run(0.01, mi)
+            ret = ctx.run(0.01, dist["max_iteration"])
             U, V = ctx.get_factors()
-        vals = {"test_rmse": O.rmse(U, V, rs.test_user_ids, rs.test_item_ids, rs.test_ratings, k),
-                "train_rmse": O.rmse(U, V, rs.user_ids, rs.item_ids, rs.ratings, k),
-                "rank_agreement": _gpu_rank_agreement(rs, U, V, k)[0], "ret": ret}
-        for m in got:
-            got[m].append(vals[m])
-        runs = [r for r in band["runs"] if r["seed"] == seed]
-        line = (f"seed {seed}: GPU ret {ret} held-out RMSE {vals['test_rmse']:.5f} (reference "
-                f"{min(r['test_rmse'] for r in runs):.5f} .. {max(r['test_rmse'] for r in runs):.5f})"
-                f" agreement {vals['rank_agreement']:.5f} (reference "
-                f"{min(r['rank_agreement'] for r in runs):.5f} .. "
-                f"{max(r['rank_agreement'] for r in runs):.5f})")
-        print(line, flush=True)
-        report.append(line)
-        for m in ("test_rmse", "rank_agreement"):
-            lo, hi = min(r[m] for r in runs), max(r[m] for r in runs)
-            assert lo - chaos[m] <= vals[m] <= hi + chaos[m], (seed, m, vals[m], lo, hi, chaos[m])
-    warnings.warn("headline-shape band (k=64, 4 ALS iterations, %d reference runs; within-seed "
-                  "chaos W: RMSE %.5f, agreement %.5f): " % (len(band["runs"]), chaos["test_rmse"],
-                                                              chaos["rank_agreement"])
-                  + "; ".join(report))
-    for m in ("test_rmse", "rank_agreement"):
-        assert pool[m][0] <= np.mean(got[m]) <= pool[m][1], (m, got[m], pool[m])
-    # the distributional statement of tests/test_gpu_parity_dist.py at the
-    # headline shape (5 GPU seeds against 30 reference runs: low power, but
-    # the same two-sided test and threshold)
-    import dist_stats as DS
-    sample = [dict({m: got[m][j] for m in got}, seed=seeds[j]) for j in range(len(seeds))]
-    res = DS.compare(sample, band["runs"])
-    print("headline shape: " + DS.describe(res), flush=True)
-    warnings.warn("headline-shape distribution: " + DS.describe(res))
-    assert not DS.failing(res), DS.describe(res)
+        got.append(dict(seed=seed, ret=ret,
+                        test_rmse=O.rmse(U, V, rs.test_user_ids, rs.test_item_ids,
+                                         rs.test_ratings, k),
+                        train_rmse=O.rmse(U, V, rs.user_ids, rs.item_ids, rs.ratings, k),
+                        rank_agreement=_gpu_rank_agreement(rs, U, V, k)[0]))
+        print("headline seed", got[-1], flush=True)
+    res = DS.compare(got, pool)
+    msg = (f"headline config (ML-full shape, k=64, own stop), {len(got)} GPU seeds vs "
+           f"{len(pool)} reference runs: " + DS.describe(res))
+    print(msg, flush=True)
+    warnings.warn(msg)
+    assert not DS.failing(res), msg
+    for m in ("test_rmse", "train_rmse"):
+        rng, W = DS.seed_ranges(pool, m)
+        for g in got:
+            lo, hi = rng[g["seed"]]
+            assert lo - W <= g[m] <= hi + W, (m, g, lo, hi, W)
 
 
 def test_predict_matches_reference_formula(gpu):

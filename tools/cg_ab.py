@@ -35,6 +35,10 @@ ap.add_argument("--tag", default="")
 ap.add_argument("--opt", action="append", default=[],
                 help="engine option NAME=VALUE (engine.OPTIONS), repeatable")
 ap.add_argument("--shard", default=None, help="R/N: rank R's share of an N-rank run")
+ap.add_argument("--wall", action="store_true",
+                help="also time the CG iteration WITHOUT per-launch events: host wall "
+                     "time of reps half-steps at m and at 2m fixed CG iterations, "
+                     "(T(2m) - T(m)) / (reps m) -- the Gram and the per-call overheads cancel")
 a = ap.parse_args()
 rs = load_data("ml-full", a.k)
 rng = np.random.RandomState(0)
@@ -77,4 +81,18 @@ with make() as ctx:
                      "gram_ms": round(st["phase_ms"]["gram_" + side] / a.reps, 4),
                      "kernels": {c: round(st["kernel_ms"][c] / max(1, st["kernel_launches"][c]) * 1e3, 2)
                                  for c in st["kernel_ms"] if st["kernel_launches"][c]}}
+    if a.wall:
+        import time
+        for side in ("users", "items"):
+            T = {}
+            for m in (a.m, 2 * a.m):
+                ctx.half_step(side, -1e300, m)   # warm
+                ctx.sync()
+                t0 = time.perf_counter()
+                for _ in range(a.reps):
+                    ctx.half_step(side, -1e300, m)
+                ctx.sync()
+                T[m] = time.perf_counter() - t0
+            out[side]["wall_ms_per_cg_iteration"] = round((T[2 * a.m] - T[a.m]) * 1e3
+                                                          / (a.reps * a.m), 4)
 print(json.dumps(out), flush=True)
