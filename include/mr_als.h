@@ -261,6 +261,10 @@ int mr_als_get_cg_vectors(mr_als* ctx, int side, double* r, double* p, double* q
  * rating range [begin, begin+len) of local entity `entity`, slab >= 0 for a
  * chunk of a split entity).  Any pointer may be NULL.  Tests. */
 long long mr_als_work_items(mr_als* ctx, int side);
+/* Grid (workgroups) of a side's CG iteration kernels as launched: kind 0 the
+ * one-pass kernel, 1 the resident solve (0: not available); nt 0 / 1 the
+ * default-policy / non-temporal tile-load instantiation. */
+int mr_als_cg_grid(mr_als* ctx, int side, int kind, int nt);
 /* This context's entities of `side`: the first global id, how many (a shard
  * owns a contiguous range) and the ratings its CSR holds.  Any may be NULL. */
 int mr_als_local_size(mr_als* ctx, int side, long long* first, long long* count,

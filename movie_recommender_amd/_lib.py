@@ -143,6 +143,7 @@ SIGNATURES = {
     "mr_als_iterate": (ctypes.c_int, [VP, ctypes.c_int]),
     "mr_als_half_step": (ctypes.c_int, [VP, ctypes.c_int, DP]),
     "mr_als_work_items": (ctypes.c_longlong, [VP, ctypes.c_int]),
+    "mr_als_cg_grid": (ctypes.c_int, [VP, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "mr_als_local_size": (ctypes.c_int, [VP, ctypes.c_int, LLP, LLP, LLP]),
     "mr_als_get_layout": (ctypes.c_int, [VP, ctypes.c_int, LLP, IP, FP, LLP, IP, IP, IP]),
     "mr_als_init_factors": (ctypes.c_int, [VP, ctypes.c_ulonglong]),

@@ -388,6 +388,12 @@ int mr_als_local_size(mr_als* ctx, int side, long long* first, long long* count,
   return 0;
 }
 
+int mr_als_cg_grid(mr_als* ctx, int side, int kind, int nt) {
+  MR_CHECK(ctx && (kind == 0 || kind == 1) && (nt == 0 || nt == 1), "bad argument");
+  const mr::Side& S = side == MR_SIDE_USERS ? ctx->eng.su : ctx->eng.si;
+  return kind == 0 ? S.n_part_op[nt] : S.n_part_rs[nt];
+}
+
 long long mr_als_work_items(mr_als* ctx, int side) {
   if (!ctx) return -1;
   return side == MR_SIDE_USERS ? ctx->eng.su.n_work : ctx->eng.si.n_work;

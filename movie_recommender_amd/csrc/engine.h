@@ -99,6 +99,8 @@ struct Engine {
   bool onepass = true;      // one kernel per CG iteration (MR_OPT_CG_ONEPASS)
   bool resident = true;     // one-pass solves as one resident launch (MR_OPT_CG_RESIDENT)
   uint64_t* d_resgen = nullptr;   // the resident solve's generation words
+  ResCtl* d_resctl = nullptr;     // its control block (write_res_ctl)
+  int write_res_ctl();
   bool rhs_mfma = true;     // user-side rhs on the matrix cores (MR_OPT_GRAM_RHS_MFMA)
   int sweep = 1;            // one-pass sweep direction per iteration (MR_OPT_CG_SWEEP)
   int tile_nt = -1;         // one-pass G tile loads: -1 by size, 0 default policy, 1

@@ -75,7 +75,7 @@ Engine::~Engine() {
       dfree(A->send, stream); dfree(A->recv, stream); dfree(A->rb, stream);
     }
     dfree(d_state, stream); dfree(partials, stream); dfree(d_flag, stream); dfree(xbins, stream);
-    dfree(d_resgen, stream);
+    dfree(d_resgen, stream); dfree(d_resctl, stream);
     dfree(d_peer, stream);
     for (void* q : peer_opened) (void)hipIpcCloseMemHandle(q);
     if (peer_buf) (void)hipFree(peer_buf);
@@ -400,10 +400,11 @@ int Engine::init(int dev, int k_, int64_t U_, int64_t I_, int64_t n_u,
   MR_HIP(hipHostGetDevicePointer((void**)&d_mirror, h_mirror, 0));
   if (dalloc(&d_state, 1, stream) || dalloc(&partials, 4 * kMaxParts, stream) ||
       dalloc(&d_flag, 4, stream) || dalloc(&xbins, kXBinWords + kXBinStartWords, stream) ||
-      dalloc(&d_resgen, kResGenWords, stream))
+      dalloc(&d_resgen, kResGenWords, stream) || dalloc(&d_resctl, 1, stream))
     return -1;
   MR_HIP(hipMemsetAsync(xbins, 0, (kXBinWords + kXBinStartWords) * sizeof(int64_t), stream));
   MR_HIP(hipMemsetAsync(d_resgen, 0, kResGenWords * sizeof(uint64_t), stream));
+  if (write_res_ctl()) return -1;
   // every field defined before any kernel reads it: the fused CG start
   // re-initialises the scalars but not `peer` (set only by set_peer)
   MR_HIP(hipMemsetAsync(d_state, 0, sizeof(CgState), stream));
@@ -645,6 +646,10 @@ int Engine::set_peer_timeout(double seconds) {
     const uint64_t ticks = (uint64_t)(seconds * 1e8);
     MR_H2D((char*)d_peer + offsetof(PeerComm, timeout_ticks), &ticks, sizeof(ticks), stream);
     MR_HIP(hipStreamSynchronize(stream));
+  }
+  if (d_resctl) {   // the resident broadcast outwaits the peers
+    MR_HIP(hipSetDevice(device));
+    if (drain() || write_res_ctl()) return -1;
   }
   return 0;
 }
@@ -918,6 +923,15 @@ CgStart Engine::cg_start_of(Side& S) {
   cs.parts = S.start_parts;
   cs.xbins = onepass_for(S) ? xbins + kXBinWords : nullptr;
   return cs;
+}
+
+// The resident solve's control block: pointers fixed for the context's
+// life, and the broadcast timeout (the peer timeout plus 30 s, rewritten
+// when that changes).
+int Engine::write_res_ctl() {
+  ResCtl c{d_state, xbins, d_resgen, d_mirror, (uint64_t)((peer_timeout_s + 30.0) * 1e8)};
+  MR_H2D(d_resctl, &c, sizeof(ResCtl), stream);
+  return 0;
 }
 
 bool Engine::resident_for(const Side& S) const {
@@ -1214,11 +1228,10 @@ int Engine::cg_onepass(Side& S, double min_dec, int max_it, double* final_rr, bo
     const bool nt = tile_nt_for(S);
     const int seq = ++mirror_seq;
     const int cls = user ? MR_K_CG_RES_USERS : MR_K_CG_RES_ITEMS;
-    const uint64_t tmo = (uint64_t)((peer_timeout_s + 30.0) * 1e8);   // 100 MHz ticks
     if (tic(cls, -1, &a)) return -1;
-    if (launch_cg_resident(stream, user, d_state, started ? 1 : 0, sweep, S.E, k, S.G, S.Gs, S.Gn,
-                           S.p, S.pb, S.r, S.rb, S.q, S.qb, xf, xb, xbins, d_resgen,
-                           S.n_part_rs[nt ? 1 : 0], d_mirror, seq, nt, tmo))
+    if (launch_cg_resident(stream, user, d_resctl, started ? 1 : 0, sweep, S.E, k, S.G, S.Gs,
+                           S.Gn, S.p, S.pb, S.r, S.rb, S.q, S.qb, xf, xb, S.n_part_rs[nt ? 1 : 0],
+                           seq, nt))
       return -1;
     if (toc(cls, -1, a)) return -1;
     const long long pend = timing ? (long long)pending.size() - 1 : -1;

@@ -1030,12 +1030,21 @@ struct RowSrc {
   __amdgpu_buffer_rsrc_t rsrc;    // BUF path: whole table
   uint32_t colb;                  // BUF path: this lane's column offset, bytes
 };
+// Timing probes of the Gram's streams (wrong results; never in the product
+// build): MR_PROBE_GRAM 1 drops the G stores, 2 the row gathers (each row
+// replaced by a value derived from its id, so the id / weight stream stays)
+#ifndef MR_PROBE_GRAM
+#define MR_PROBE_GRAM 0
+#endif
 template <int NB, int T, bool BUF>
 __device__ __forceinline__ void gather_row(float (&f)[8][NB], float (&w)[8], ChunkRegs cr,
                                            const RowSrc& src, uint32_t row_bytes) {
   const int ri = row_bcast<T>(cr.idx);
   w[T] = __builtin_bit_cast(float, row_bcast<T>(__builtin_bit_cast(int, cr.w)));
-  if constexpr (BUF) {
+  if constexpr (MR_PROBE_GRAM == 2) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) f[T][b] = (float)(ri + b) * 1e-6f;
+  } else if constexpr (BUF) {
     const uint32_t off = (uint32_t)ri * row_bytes + src.colb;
 #pragma unroll
     for (int h = 0; h < NB / 4; ++h) {
@@ -1231,6 +1240,7 @@ __device__ __forceinline__ void bf3_mfma(floatx4 (&acc)[NB * (NB + 1) / 2], floa
 #define MR_G_NT 1
 #endif
 __device__ __forceinline__ void gst(float* p, float v) {
+  if (MR_PROBE_GRAM == 1) return;
   if (MR_G_NT) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
@@ -3066,23 +3076,26 @@ __device__ __forceinline__ void op_load(const OpSide& A, int64_t e, int update, 
   const double* re = A.r + e * A.ldk;
   const double* qe = A.q + e * A.ldk;
   const float* xe = A.x + e * A.ldk;
+  // q and x are loaded whether or not this iteration applies the deferred
+  // update (only the first iteration of an unfused start does not; their
+  // values are then unused): a load under a branch made the compiler wait
+  // for it inside the branch, ahead of the G tile loads
+  (void)update;
 #pragma unroll
   for (int h = 0; h < T::NV; ++h) {
     const int i = lane + 64 * h;
     E_.pi[h] = (i < T::NP) ? pe[i] : 0.0;
     E_.ri[h] = (i < T::NP) ? re[i] : 0.0;
-    E_.qi[h] = (update && i < T::NP) ? qe[i] : 0.0;
-    E_.xi[h] = (update && i < T::NP) ? xe[i] : 0.f;
+    E_.qi[h] = (i < T::NP) ? qe[i] : 0.0;
+    E_.xi[h] = (i < T::NP) ? xe[i] : 0.f;
   }
   E_.pbias = E_.rbias = E_.qbias = 0.0;
   E_.xbias = 0.f;
   if (USER) {
     E_.pbias = A.pb[e];
     E_.rbias = A.rb[e];
-    if (update) {
-      E_.qbias = A.qb[e];
-      E_.xbias = A.xb[e];
-    }
+    E_.qbias = A.qb[e];
+    E_.xbias = A.xb[e];
   }
   const floatx4* __restrict__ Ge = reinterpret_cast<const floatx4*>(A.G + e * T::GS);
   if constexpr (T::STREAM) {
@@ -3091,8 +3104,12 @@ __device__ __forceinline__ void op_load(const OpSide& A, int64_t e, int update, 
 #pragma unroll
     for (int t = 0; t < T::NTILE; ++t) E_.g[t] = tile_ld<NT>(Ge, t, lane);
   }
-  E_.d2 = 0.f;
-  if (T::NF > 0 && lane < 16 * T::NF) E_.d2 = A.G[e * T::GS + T::NTILE * 256 + lane];
+  // the folded tiles' side diagonals (lanes < 16 NF use them); every lane
+  // loads (a clamped index), so no register is zeroed and then loaded under
+  // an exec mask -- that pattern made the wait-count pass drain every load
+  // in flight at the next entity's start
+  if constexpr (T::NF > 0) E_.d2 = A.G[e * T::GS + T::NTILE * 256 + (lane < 16 * T::NF ? lane : 0)];
+  else E_.d2 = 0.f;
 }
 
 // Entity e of one CG iteration (matrix.cpp:488-526 in block form): the
@@ -3356,19 +3373,58 @@ __device__ __forceinline__ void store_state_sc1(CgState* st, const CgScalars& v)
   s(&st->sharded, v.sharded);
 }
 
-// MR_RS_PREFETCH 1: each wave loads its first entity of iteration t + 1
-// while it waits for iteration t's broadcast (holds the operands across the
-// barrier)
+// While a wave waits for iteration t's broadcast, its first entity of
+// iteration t + 1 can already be on its way (MR_RS_PREFETCH): 1 loads its
+// operands into registers (held across the barrier), 2 "touches" every
+// 128-byte line of its G tiles and vectors with one dword load per lane
+// (results discarded: the lines come into L2, no operand registers held),
+// 3 = registers where they fit (NB > 4: 2 waves per SIMD) and touches
+// below; 0 none.
 #ifndef MR_RS_PREFETCH
 #define MR_RS_PREFETCH 0
 #endif
+// poll interval of the broadcast wait (s_sleep units of 64 clocks): one
+// poller per block, 4 blocks per CU
+#ifndef MR_RS_SLEEP
+#define MR_RS_SLEEP 1
+#endif
+__device__ __forceinline__ uint32_t touch_lines(const void* p, int64_t nbytes, int lane) {
+  uint32_t s = 0;
+  for (int64_t o = (int64_t)lane * 128; o < nbytes; o += 64 * 128)
+    s += *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(p) + o);
+  return s;
+}
+template <int NB, bool USER>
+__device__ __forceinline__ uint32_t op_touch(const OpSide& A, int64_t e, int lane) {
+  using T = OpEnt<NB>;
+  uint32_t s = touch_lines(A.G + e * T::GS, T::GS * 4, lane);
+  s += touch_lines(A.p + e * A.ldk, A.ldk * 8, lane);
+  s += touch_lines(A.r + e * A.ldk, A.ldk * 8, lane);
+  s += touch_lines(A.q + e * A.ldk, A.ldk * 8, lane);
+  s += touch_lines(A.x + e * A.ldk, A.ldk * 4, lane);
+  return s;
+}
+// The resident solve's control words live in device memory (ResCtl,
+// Engine-owned) and are loaded where they are used, through a pointer made
+// opaque at each use: kept in SGPRs for the whole kernel, the barrier's
+// pointers pushed the one-pass body into SGPR spills (49 SGPRs into VGPR
+// lanes, ~110 v_readlane in the loop) and its loads behind vmcnt(0) waits
+// (users k = 64 full size: 207 vs 196 us per CG iteration).
+template <class P>
+__device__ __forceinline__ P* opaque_ptr(P* p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
+#ifndef MR_RS_WAVES
+#define MR_RS_WAVES MR_OP_WAVES
+#endif
 template <int NB, bool USER, bool NT>
-__global__ __launch_bounds__(256, (NB <= 4 ? (USER && NB == 4 ? MR_OP_WAVES_U4 : MR_OP_WAVES) : 2))
-void cg_resident_kernel(CgState* __restrict__ st, int t0, int sweep, OpSide A,
-                        int64_t* __restrict__ xbins, uint64_t* __restrict__ gen,
-                        CgMirror* mirror, int seq, uint64_t tmo) {
+__global__ __launch_bounds__(256, (NB <= 4 ? MR_RS_WAVES : 2))
+void cg_resident_kernel(const ResCtl* __restrict__ ctl, int t0, int sweep, int seq, OpSide A) {
   constexpr int XC = xchunk_of(NB, USER);
   using T = OpEnt<NB>;
+  constexpr int PF = MR_RS_PREFETCH == 3 ? (NB > 4 ? 1 : 2) : MR_RS_PREFETCH;
   __shared__ MvScratch<NB> scr[MV_WAVES];
   __shared__ double rvs[MV_WAVES][16 * NB];
   __shared__ int64_t xacc[1][4][kXW];
@@ -3376,79 +3432,104 @@ void cg_resident_kernel(CgState* __restrict__ st, int t0, int sweep, OpSide A,
   __shared__ int s_flag[2];   // [0]: broadcast done (2: failed), [1]: last block
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wu = __builtin_amdgcn_readfirstlane(wid);
-  const int64_t nch = (A.E + XC - 1) / XC;
-  const int64_t j0 = (int64_t)blockIdx.x * MV_WAVES + wu, js = (int64_t)gridDim.x * MV_WAVES;
-  const int64_t cnt = j0 < nch ? (nch - 1 - j0) / js + 1 : 0;   // chunks this wave owns
+  // chunk counts fit 32 bits (E < 2^31 entities)
+  const int nch = (int)((A.E + XC - 1) / XC);
+  const int j0 = (int)blockIdx.x * MV_WAVES + wu, js = (int)gridDim.x * MV_WAVES;
+  const int cnt = j0 < nch ? (nch - 1 - j0) / js + 1 : 0;   // chunks this wave owns
   // the i-th chunk of a sweep: ascending, or descending on reversed sweeps
   // (MR_OPT_CG_SWEEP: 1 = iteration 1 backwards, then alternate)
   auto rev_of = [&](int t) { return sweep == 0 ? 0 : ((t & 1) ^ (sweep == 2 ? 1 : 0)); };
-  auto chunk0 = [&](int64_t i, int rev) { return (j0 + (rev ? cnt - 1 - i : i) * js) * XC; };
+  auto chunk0 = [&](int i, int rev) { return (int64_t)(j0 + (rev ? cnt - 1 - i : i) * js) * XC; };
   // the state at entry was written by the previous kernels of the stream
-  double alpha = ald(&st->alpha), beta = ald(&st->beta);
-  int done = ald(&st->done);
+  CgState* st0 = opaque_ptr(ctl)->st;
+  double alpha = ald(&st0->alpha), beta = ald(&st0->beta);
+  int done = ald(&st0->done);
   if (threadIdx.x < 4 * kXW) (&xacc[0][0][0])[threadIdx.x] = 0;
   if (done) {
     // ended at the start: publish for the host; the start's pending update
-    if (blockIdx.x == 0 && threadIdx.x == 0) publish(load_state(st), mirror, seq);
-    if (!ald(&st->pending)) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) publish(load_state(st0), ctl->mirror, seq);
+    if (!ald(&st0->pending)) return;
   }
   int t = t0;
   OpEnt<NB> cur;
-  if (MR_RS_PREFETCH && !done && cnt > 0) op_load<NB, USER, NT>(A, chunk0(0, rev_of(t)), t > 0, cur, lane);
+  if (PF == 1 && !done && cnt > 0) op_load<NB, USER, NT>(A, chunk0(0, rev_of(t)), t > 0, cur, lane);
   __syncthreads();
   while (!done) {
     const int update = t > 0, rev = rev_of(t);
-    const int lo = lane;
-    MvScratch<NB>& sci = scr[wid];
-    double* rsi = rvs[wid];
-    for (int64_t i = 0; i < cnt; ++i) {
+    // MR_OP_PROF builds: the timeline of this launch's iteration t0 + 2
+    // (tools/op_timeline.py --resident): per block start / chunks done /
+    // arrival / broadcast seen; the last block's collect / compute / gen
+    const bool prof = MR_OP_PROF && t == t0 + 2;
+    if (prof && threadIdx.x == 0) op_prof(8);
+    MvScratch<NB>& sc = scr[wid];
+    double* rs = rvs[wid];
+    for (int i = 0; i < cnt; ++i) {
       const int64_t c0 = chunk0(i, rev);
       const int64_t c1 = c0 + XC < A.E ? c0 + XC : A.E;
       double a = 0.0, b = 0.0, c = 0.0, d = 0.0;
       for (int64_t e = c0; e < c1; ++e) {
-        if (!MR_RS_PREFETCH || i != 0 || e != c0) op_load<NB, USER, NT>(A, e, update, cur, lo);
-        op_process<NB, USER, NT>(A, e, update, alpha, beta, cur, sci, rsi, a, b, c, d, lo);
+        if constexpr (PF == 1) {
+          if (i != 0 || e != c0) op_load<NB, USER, NT>(A, e, update, cur, lane);
+          op_process<NB, USER, NT>(A, e, update, alpha, beta, cur, sc, rs, a, b, c, d, lane);
+        } else {
+          OpEnt<NB> en;
+          op_load<NB, USER, NT>(A, e, update, en, lane);
+          op_process<NB, USER, NT>(A, e, update, alpha, beta, en, sc, rs, a, b, c, d, lane);
+        }
       }
-      op_chunk_terms(a, b, c, d, xacc, lo);
+      op_chunk_terms(a, b, c, d, xacc, lane);
     }
     // the block's containers into the bins (and cleared for the next
     // iteration by the thread that read them), then the arrival.  Every
     // thread-derived address below comes from a fresh opaque copy of the
     // thread index: hoisted out of the iteration loop, these addresses would
     // stay live across the GEMV (17 VGPRs spilled at NB = 4)
+    if (prof && (threadIdx.x & 63) == 0) op_prof(9);   // the block's last wave wins
     __syncthreads();
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));
+    const ResCtl* C = opaque_ptr(ctl);
+    CgState* st = C->st;
     if (tid < 4 * kXW) {
       const int v = tid / kXW, dd = tid % kXW;
       const int64_t tt = xacc[0][v][dd];
       xacc[0][v][dd] = 0;
       if (tt != 0)
-        __hip_atomic_fetch_add(xbins + ((int64_t)(blockIdx.x % kXBins) * 4 + v) * kXW + dd, tt,
+        __hip_atomic_fetch_add(C->xbins + ((int64_t)(blockIdx.x % kXBins) * 4 + v) * kXW + dd, tt,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (threadIdx.x == 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       s_flag[1] = __hip_atomic_fetch_add(&st->arrive, 1u, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+      if (prof) op_prof(10);
     }
     __syncthreads();
     const bool fin = s_flag[1] && wid == 0;
     const uint64_t want = ((uint64_t)(uint32_t)seq << 32) | (uint32_t)(t + 1);
-    // this wave's own stores of the iteration are complete before it
-    // re-reads its first entity's vectors for the next one
-    if (MR_RS_PREFETCH) {
+    uint32_t touched = 0;
+    if (PF == 1) {
+      // this wave's own stores of the iteration are complete before it
+      // re-reads its first entity's vectors for the next one
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (!fin && cnt > 0) op_load<NB, USER, NT>(A, chunk0(0, rev_of(t + 1)), 1, cur, lane);
+    } else if (PF == 2 && !fin && cnt > 0) {
+      touched = op_touch<NB, USER>(A, chunk0(0, rev_of(t + 1)), tid & 63);
     }
+#ifndef MR_RSX_NOFIN
     if (fin) {
+#else
+    if (false) {
+#endif
       __shared__ int64_t xs[4 * kXW];
       __shared__ double xv[4];
       const int lane = tid & 63;
       PeerComm* pc = ald(&st->peer);
       CgScalars v{};
       if (lane == 0) v = load_state_sc1(st);
-      int64_t tot = xsum_collect<4>(xbins, lane);
+      if (prof && lane == 0) op_prof(0);
+      int64_t tot = xsum_collect<4>(C->xbins, lane);
+      if (prof && lane == 0) op_prof(1);
       if (lane == 0) __hip_atomic_store(&st->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       int flag = 0;
       if (pc && !peer_sum_lanes(pc, tot, 4 * kXW)) {
@@ -3456,7 +3537,7 @@ void cg_resident_kernel(CgState* __restrict__ st, int t0, int sweep, OpSide A,
           v.done = 1;
           v.ret = -1;
           store_state_sc1(st, v);
-          publish(v, mirror, seq);
+          publish(v, C->mirror, seq);
         }
         flag = 2;
       } else {
@@ -3471,7 +3552,7 @@ void cg_resident_kernel(CgState* __restrict__ st, int t0, int sweep, OpSide A,
           op_beta(v, sum, update);
           store_state_sc1(st, v);
           __hip_atomic_store(&st->pending, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (v.done) publish(v, mirror, seq);
+          if (v.done) publish(v, C->mirror, seq);
           flag = v.done;
         }
       }
@@ -3480,16 +3561,21 @@ void cg_resident_kernel(CgState* __restrict__ st, int t0, int sweep, OpSide A,
         __hip_atomic_store(&st->res_beta, v.beta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&st->res_done, flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      if (prof && lane == 0) op_prof(2);
       // every store above (state, broadcast, the bins' clears) written
       // through and drained before the generation word moves
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane < kResGenCopies)
-        __hip_atomic_store(gen + lane * kResGenStride, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(C->gen + lane * kResGenStride, want, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (MR_RS_PREFETCH && cnt > 0) op_load<NB, USER, NT>(A, chunk0(0, rev_of(t + 1)), 1, cur, lane);
+      if (prof && lane == 0) op_prof(3);
+      if (PF == 1 && cnt > 0) op_load<NB, USER, NT>(A, chunk0(0, rev_of(t + 1)), 1, cur, lane);
+      if (PF == 2 && cnt > 0) touched = op_touch<NB, USER>(A, chunk0(0, rev_of(t + 1)), lane);
     }
     if (threadIdx.x == 0) {
-      const uint64_t* g = gen + (blockIdx.x % kResGenCopies) * kResGenStride;
+      const uint64_t* g = C->gen + (blockIdx.x % kResGenCopies) * kResGenStride;
+      const uint64_t tmo = C->timeout_ticks;
       const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
       int ok = 1;
       while (__hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
@@ -3497,22 +3583,24 @@ void cg_resident_kernel(CgState* __restrict__ st, int t0, int sweep, OpSide A,
           ok = 0;
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(MR_RS_SLEEP);
       }
+      if (prof) op_prof(11);
       s_ab[0] = __hip_atomic_load(&st->res_alpha, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_ab[1] = __hip_atomic_load(&st->res_beta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_flag[0] = ok ? __hip_atomic_load(&st->res_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 2;
     }
     __syncthreads();
+    if (PF == 2) asm volatile("" ::"v"(touched));   // the touches are not dead code
     // wave-uniform values back into scalar registers (LDS loads land in VGPRs)
     alpha = __builtin_bit_cast(double, ((int64_t)__builtin_amdgcn_readfirstlane(
-                                           (int)__builtin_bit_cast(int64_t, s_ab[0])) & 0xFFFFFFFFll) |
-                                       (int64_t)__builtin_amdgcn_readfirstlane(
-                                           (int)(__builtin_bit_cast(int64_t, s_ab[0]) >> 32)) << 32);
+                                            (int)__builtin_bit_cast(int64_t, s_ab[0])) & 0xFFFFFFFFll) |
+                                           (int64_t)__builtin_amdgcn_readfirstlane(
+                                               (int)(__builtin_bit_cast(int64_t, s_ab[0]) >> 32)) << 32);
     beta = __builtin_bit_cast(double, ((int64_t)__builtin_amdgcn_readfirstlane(
-                                          (int)__builtin_bit_cast(int64_t, s_ab[1])) & 0xFFFFFFFFll) |
-                                      (int64_t)__builtin_amdgcn_readfirstlane(
-                                          (int)(__builtin_bit_cast(int64_t, s_ab[1]) >> 32)) << 32);
+                                           (int)__builtin_bit_cast(int64_t, s_ab[1])) & 0xFFFFFFFFll) |
+                                          (int64_t)__builtin_amdgcn_readfirstlane(
+                                              (int)(__builtin_bit_cast(int64_t, s_ab[1]) >> 32)) << 32);
     done = __builtin_amdgcn_readfirstlane(s_flag[0]);
     if (done == 2) return;   // failed peer exchange or a broadcast that never came
     ++t;
@@ -3520,7 +3608,8 @@ void cg_resident_kernel(CgState* __restrict__ st, int t0, int sweep, OpSide A,
   }
   // the stopped iteration's x update (UPD_FINISH), entry by entry on this
   // wave's own entities: x += alpha p (its residual update would be dead)
-  for (int64_t i = 0; i < cnt; ++i) {
+#ifndef MR_RSX_NOFINISH
+  for (int i = 0; i < cnt; ++i) {
     const int64_t c0 = chunk0(i, 0);
     const int64_t c1 = c0 + XC < A.E ? c0 + XC : A.E;
     for (int64_t e = c0; e < c1; ++e) {
@@ -3535,6 +3624,7 @@ void cg_resident_kernel(CgState* __restrict__ st, int t0, int sweep, OpSide A,
       if (USER && lane == 0) A.xb[e] = (float)fma(alpha, A.pb[e], (double)A.xb[e]);
     }
   }
+#endif
 }
 
 // MR_OP_PROF builds: copy the last one-pass launch's timeline out (slots 0-3:
@@ -3612,16 +3702,14 @@ int resident_blocks_per_cu(bool user_side, int k, bool nt) {
   return n;
 }
 
-int launch_cg_resident(hipStream_t s, bool user_side, CgState* st, int t0, int sweep, int64_t E,
-                       int k, const float* G, const float* Gs, const float* Gn, double* p,
+int launch_cg_resident(hipStream_t s, bool user_side, const ResCtl* ctl, int t0, int sweep,
+                       int64_t E, int k, const float* G, const float* Gs, const float* Gn, double* p,
                        double* pb, double* r, double* rb, double* q, double* qb, float* x,
-                       float* xb, int64_t* xbins, uint64_t* gen, int n_part, CgMirror* mirror,
-                       int seq, bool nt, uint64_t timeout_ticks) {
+                       float* xb, int n_part, int seq, bool nt) {
   if (n_part <= 0) return 0;
   const OpSide A{E, k, ldk_of(k), G, Gs, Gn, p, pb, r, rb, q, qb, x, xb};
 #define MR_RS_LAUNCH(NB, U, T)                                                              \
-  MR_LAUNCH((cg_resident_kernel<NB, U, T>), dim3(n_part), dim3(256), 0, s, st, t0, sweep, A,   \
-            xbins, gen, mirror, seq, timeout_ticks)
+  MR_LAUNCH((cg_resident_kernel<NB, U, T>), dim3(n_part), dim3(256), 0, s, ctl, t0, sweep, seq, A)
 #define MR_RS_CASE(NB)                                                                      \
   case NB:                                                                                  \
     if (user_side) {                                                                        \

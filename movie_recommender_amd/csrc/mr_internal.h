@@ -332,16 +332,22 @@ int launch_cg_onepass(hipStream_t s, bool user_side, CgState* st, int update, in
 // one solve in one launch, from iteration t0 (0: unfused start, 1: after a
 // fused start) until the stop; publishes the final state under `seq` and
 // applies the pending x update.  Needs every block of the grid resident at
-// once: n_part = resident_blocks_per_cu(...) x CUs at most.  gen:
+// once: n_part = resident_blocks_per_cu(...) x CUs at most.  ctl->gen:
 // kResGenWords uint64 (any content except a value (seq << 32) | t of this
-// launch).  timeout_ticks (100 MHz): a block whose broadcast does not come
-// gives up (the host's wait then reports the unpublished state).
+// launch).  ctl->timeout_ticks: a block whose broadcast does not come gives
+// up (the host's wait then reports the unpublished state).
+struct ResCtl {   // device memory, written by the engine (Engine::write_res_ctl)
+  CgState* st;
+  int64_t* xbins;         // kXBinWords bins of the iteration sums
+  uint64_t* gen;          // kResGenWords generation words
+  CgMirror* mirror;       // host-mapped ring the final state is published into
+  uint64_t timeout_ticks; // s_memrealtime ticks (100 MHz) a block waits for a broadcast
+};
 int resident_blocks_per_cu(bool user_side, int k, bool nt);
-int launch_cg_resident(hipStream_t s, bool user_side, CgState* st, int t0, int sweep, int64_t E,
-                       int k, const float* G, const float* Gs, const float* Gn, double* p,
+int launch_cg_resident(hipStream_t s, bool user_side, const ResCtl* ctl, int t0, int sweep,
+                       int64_t E, int k, const float* G, const float* Gs, const float* Gn, double* p,
                        double* pb, double* r, double* rb, double* q, double* qb, float* x,
-                       float* xb, int64_t* xbins, uint64_t* gen, int n_part, CgMirror* mirror,
-                       int seq, bool nt, uint64_t timeout_ticks);
+                       float* xb, int n_part, int seq, bool nt);
 // x is the fp32 factor table (and bias), r / p / q the fp64 CG vectors;
 // nt: non-temporal G tile loads (Engine::tile_nt_for);
 // xbins: kXBins x 4 x 11 int64 bins of the order-independent sums (zero

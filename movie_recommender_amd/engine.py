@@ -142,6 +142,12 @@ class AlsContext:
         return _lib.check(_lib.lib().mr_als_run(self._h, float(min_r_decrease),
                                                 int(max_iterations)), "mr_als_run")
 
+    def cg_grid(self, side, resident=False, nt=False):
+        """Workgroups of the side's CG iteration kernel (one-pass, or the
+        resident solve: 0 when unavailable) for one tile-load policy."""
+        return _lib.lib().mr_als_cg_grid(self._h, 0 if side == "users" else 1,
+                                         int(bool(resident)), int(bool(nt)))
+
     def iterate(self, n=1):
         """Exactly ``n`` ALS iterations (user + item half-step each)."""
         _lib.check(_lib.lib().mr_als_iterate(self._h, int(n)), "mr_als_iterate")

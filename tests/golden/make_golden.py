@@ -583,11 +583,11 @@ G13_TCS = (1, 2, 4)
 G13_SEEDS = 20
 
 
-def _g13_part(tc):
-    return os.path.join("/tmp", f"dist_mlfull_k64_tc{tc}.partial.json")
+def _g13_part(tc, tag=""):
+    return os.path.join("/tmp", f"dist_mlfull_k64_tc{tc}{tag}.partial.json")
 
 
-def g13(tc=None):
+def g13(tc=None, seeds=None, tag=""):
     """Round 6 (VERDICT r05 "do this" 2): the headline config's realistic-
     data distribution.  The ML-full-shaped generator at k = 64 (20 % held
     out, the data of ``g9``), initial-factor seeds 0 .. 19, the compiled
@@ -600,11 +600,11 @@ def g13(tc=None):
     k = 64
     rs_ = synth.movielens_like("ml-full", k, seed=synth.DATA_SEED, test_ratio=0.2)
     for t in tcs:
-        part = _g13_part(t)
+        part = _g13_part(t, tag)
         runs = json.load(open(part)) if os.path.exists(part) else []
         done = {r["seed"] for r in runs}
         ref.set_thread_count(t)
-        for seed in range(G13_SEEDS):
+        for seed in (seeds if seeds is not None else range(G13_SEEDS)):
             if seed in done:
                 continue
             U0, V0 = ref.init_factors(rs_.num_users, rs_.num_items, k, seed)
@@ -622,10 +622,13 @@ def g13(tc=None):
 def g13m():
     k = 64
     rs_ = synth.movielens_like("ml-full", k, seed=synth.DATA_SEED, test_ratio=0.2)
-    runs = []
-    for t in G13_TCS:
-        runs += json.load(open(_g13_part(t)))
-    runs.sort(key=lambda r: (r["seed"], r["tc"]))
+    import glob
+    got = {}
+    for t in G13_TCS:   # a thread count's seeds may come from several processes
+        for f in sorted(glob.glob(_g13_part(t, "*"))):
+            for r in json.load(open(f)):
+                got.setdefault((r["seed"], r["tc"]), r)
+    runs = sorted(got.values(), key=lambda r: (r["seed"], r["tc"]))
     assert len(runs) == G13_SEEDS * len(G13_TCS), len(runs)
     dist = dict(shape="ml-full", k=k, data_seed=synth.DATA_SEED, test_ratio=0.2,
                 max_iteration=200, n_train=int(rs_.n), n_test=int(len(rs_.test_ratings)),
@@ -646,8 +649,14 @@ if __name__ == "__main__":
     while i < len(args):
         fn = globals()[args[i]]
         if args[i] == "g13" and i + 1 < len(args) and args[i + 1].isdigit():
-            fn(args[i + 1])
-            i += 2
+            if i + 3 < len(args) and args[i + 2].isdigit() and args[i + 3].isdigit():
+                # g13 <tc> <first seed> <last seed>: a second process's share
+                lo, hi = int(args[i + 2]), int(args[i + 3])
+                fn(args[i + 1], range(lo, hi + 1), f"_s{lo}")
+                i += 4
+            else:
+                fn(args[i + 1])
+                i += 2
         else:
             fn()
             i += 1

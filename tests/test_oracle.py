@@ -115,6 +115,28 @@ def test_dist_fixture_regenerates(k):
     assert len(DS.runs_of(d, "ref")) == 6 * d["n_seeds"] and d["n_seeds"] >= 20
 
 
+def test_headline_dist_fixture_is_the_reference_pool():
+    """The headline config's pool (make_golden.py g13: the compiled reference
+    at 20 seeds x thread counts {1, 2, 4}, its own outer stop) describes the
+    data set the GPU test rebuilds, and every run stopped by the reference's
+    own rule (ret >= 3: matrix.cpp:871-875 tests from iteration 3 on, far
+    below max_iteration 200)."""
+    import json
+    from movie_recommender_amd import synth
+    with open(os.path.join(GOLDEN, "dist_mlfull_k64.json")) as f:
+        d = json.load(f)
+    runs = [r for r in d["runs"] if r["kind"] == "ref"]
+    assert d["max_iteration"] == 200 and d["k"] == 64 and d["n_seeds"] >= 20
+    assert sorted({(r["seed"], r["tc"]) for r in runs}) == sorted(
+        (s, t) for s in range(d["n_seeds"]) for t in d["thread_counts"])
+    assert len(d["thread_counts"]) >= 3
+    assert all(3 <= r["ret"] < d["max_iteration"] for r in runs)
+    rs = synth.movielens_like(d["shape"], d["k"], seed=d["data_seed"], test_ratio=d["test_ratio"])
+    assert rs.n == d["n_train"] and len(rs.test_ratings) == d["n_test"]
+    assert abs(float(np.sum(rs.ratings)) - d["ratings_checksum"]) < 1e-6
+    assert abs(float(np.sum(rs.medians)) - d["medians_checksum"]) < 1e-6
+
+
 @pytest.mark.parametrize("k", [10, 32])
 @pytest.mark.parametrize("kind", ["block64", "block32"])
 def test_restatement_distribution_matches_reference(k, kind):

@@ -16,5 +16,5 @@ OBJ=$ROOT/build/obj
   -o "$OUT/${UNIT:-kernels}.o"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC "$OUT/${UNIT:-kernels}.o" \
   $(ls $OBJ/*.o | grep -v "/${UNIT:-kernels}.o$") -o "$OUT/cpp_ls_lib.so" \
-  -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+  -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -Wl,-z,defs
 echo "$OUT/cpp_ls_lib.so"

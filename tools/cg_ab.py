@@ -63,6 +63,9 @@ with make() as ctx:
     for o in a.opt:
         name, val = o.split("=")
         ctx.set_option(name, float(val))
+    out["grid"] = {side: {"onepass": [ctx.cg_grid(side, False, nt) for nt in (0, 1)],
+                          "resident": [ctx.cg_grid(side, True, nt) for nt in (0, 1)]}
+                   for side in ("users", "items")}
     ctx.set_factors(U0, V0)
     ctx.iterate(3)
     ctx.sync()

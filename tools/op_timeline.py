@@ -27,6 +27,10 @@ ap.add_argument("--k", type=int, default=64)
 ap.add_argument("--shard", default=None)
 ap.add_argument("--side", default="users")
 ap.add_argument("--m", type=int, default=8)
+ap.add_argument("--resident", action="store_true",
+                help="the resident solve's iteration t0 + 2: per block start / chunks "
+                     "done / arrival / broadcast seen, the last block's collect / "
+                     "compute / generation store")
 a = ap.parse_args()
 rs = load_data("ml-full", a.k)
 rng = np.random.RandomState(0)
@@ -49,6 +53,7 @@ n = 8 + 4 * 4096
 buf = (ctypes.c_longlong * n)()
 out = {"k": a.k, "shard": a.shard, "side": a.side, "m": a.m}
 with ctx:
+    ctx.set_option("cg_resident", 1 if a.resident else 0)
     ctx.set_factors(U0, V0)
     for _ in range(2):
         ctx.half_step(a.side, float("-inf"), a.m)   # warm, fixed CG count
@@ -61,6 +66,14 @@ blk = blk[used]
 t0 = blk[:, 0].min()
 us = lambda x: round(float(x - t0) / 100.0, 2)  # noqa: E731  (100 MHz ticks)
 out["blocks"] = int(used.sum())
+if a.resident:
+    q = lambda col: {"min": us(blk[:, col].min()), "median": us(np.median(blk[:, col])),  # noqa
+                     "p90": us(np.percentile(blk[:, col], 90)), "max": us(blk[:, col].max())}
+    out.update({"chunks_done_us": q(1), "arrived_us": q(2), "broadcast_seen_us": q(3),
+                "last_block_us": {"collect_start": us(t[0]), "collected": us(t[1]),
+                                  "computed": us(t[2]), "gen_stored": us(t[3])}})
+    print(json.dumps(out))
+    sys.exit(0)
 out["entry_us"] = {"min": 0.0, "median": us(np.median(blk[:, 0])), "max": us(blk[:, 0].max())}
 out["entities_done_us"] = {"min": us(blk[:, 1].min()), "median": us(np.median(blk[:, 1])),
                            "max": us(blk[:, 1].max())}
