@@ -3432,7 +3432,12 @@ void cg_resident_kernel(const ResCtl* __restrict__ ctl, int t0, int sweep, int s
   __shared__ int s_flag[2];   // [0]: broadcast done (2: failed), [1]: last block
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wu = __builtin_amdgcn_readfirstlane(wid);
-  // chunk counts fit 32 bits (E < 2^31 entities)
+  // Wave j0 owns chunks j0, j0 + js, j0 + 2 js, ... (the one-pass deal,
+  // fixed for the whole solve; its order reversed on alternate sweeps), so
+  // at any moment the grid works on one contiguous window of the side.  A
+  // deal of contiguous ranges per wave (counts balanced over the CUs) was
+  // measured 10 % slower at full size and no better at shard 0/8
+  // (profiles/r06/r06g).  Chunk counts fit 32 bits (E < 2^31 entities).
   const int nch = (int)((A.E + XC - 1) / XC);
   const int j0 = (int)blockIdx.x * MV_WAVES + wu, js = (int)gridDim.x * MV_WAVES;
   const int cnt = j0 < nch ? (nch - 1 - j0) / js + 1 : 0;   // chunks this wave owns
@@ -3568,7 +3573,8 @@ void cg_resident_kernel(const ResCtl* __restrict__ ctl, int t0, int sweep, int s
       if (lane < kResGenCopies)
         __hip_atomic_store(C->gen + lane * kResGenStride, want, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // (no drain here: this block's own poll below simply repeats until
+      // its generation store is visible)
       if (prof && lane == 0) op_prof(3);
       if (PF == 1 && cnt > 0) op_load<NB, USER, NT>(A, chunk0(0, rev_of(t + 1)), 1, cur, lane);
       if (PF == 2 && cnt > 0) touched = op_touch<NB, USER>(A, chunk0(0, rev_of(t + 1)), lane);
