@@ -408,7 +408,8 @@ def main():
                          "(e.g. 0,0 puts two ranks on GPU 0; needs --comm gloo)")
     ap.add_argument("--pmc", default=None,
                     help="per-kernel HBM bytes from a rocprofv3 --pmc run (optional; default "
-                         "profiles/pmc_r05.json at k = 64, profiles/pmc_r05_k<k>.json otherwise; r04 if absent)")
+                         "profiles/pmc_r06.json at k = 64, profiles/pmc_r06_k<k>.json otherwise; the "
+                         "previous round's if absent)")
     args = ap.parse_args()
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -692,7 +693,7 @@ def main():
     traffic = None
     pmc_path = args.pmc
     if not pmc_path:   # this round's counter passes, else the previous round's
-        for rnd in ("r05", "r04"):
+        for rnd in ("r06", "r05", "r04"):
             pmc_path = os.path.join(ROOT, "profiles",
                                     f"pmc_{rnd}.json" if k == 64 else f"pmc_{rnd}_k{k}.json")
             if os.path.exists(pmc_path):
@@ -703,7 +704,14 @@ def main():
         # only for the workload the counter passes ran (per-launch bytes)
         wl = pmc.get("workload", {"shape": "ml-full", "k": 64})
         if wl.get("shape") == args.shape and wl.get("k") == k and world == 1 and not c5:
-            traffic = pmc.get("hbm_bytes_per_launch", {}).get(cls)
+            per = pmc.get("hbm_bytes_per_launch", {})
+            traffic = per.get(cls)
+            if traffic is None and cls.startswith("resident_"):
+                # the resident solve's iterations make the launch-per-iteration
+                # kernel's accesses (the counter passes run that path:
+                # per-launch = per CG iteration) times its iterations per launch
+                it = per.get("matvec_" + cls[len("resident_"):])
+                traffic = None if it is None else int(it * units_per_launch)
     kernel_table = {}
     for c, ms in st["kernel_ms"].items():
         n = st["kernel_launches"][c]

@@ -990,7 +990,7 @@ __device__ __forceinline__ void start_from_acc(const floatx4 (&acc)[NB * (NB + 1
 // hl + lh + mm (the dropped ml, lm, ll are <= 2^-24 relative, below the fp32
 // rounding of the sum).
 // ---------------------------------------------------------------------------
-constexpr int GRAM_WAVES = 4;
+
 
 // Per-lane raw loads of one 32-rating half: opposite id, rating and (item
 // side) the opposite bias.  Lanes past the end of the work item load from a
@@ -1450,7 +1450,7 @@ __device__ __forceinline__ void gram_wave(
 // (start_from_acc; split entities are started after slab_reduce) and meet
 // once at the end to store the block's (r.r, p.Gp) pair.
 template <int NB, bool USER, bool FUSE, bool BUF, bool RHSM>
-__global__ __launch_bounds__(256, (NB <= 4 ? 3 : 1)) void gram_kernel(
+__global__ __launch_bounds__(64 * GRAM_WAVES, (NB <= 4 ? 3 : 1)) void gram_kernel(
     const WorkItem* __restrict__ work, int64_t n_work,
     const int32_t* __restrict__ idx, const float* __restrict__ val,
     const float* __restrict__ F, const float* __restrict__ bias, int k, int ldk, int zrow,

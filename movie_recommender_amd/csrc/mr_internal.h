@@ -294,8 +294,13 @@ int launch_gram(hipStream_t s, bool user_side, int k, const WorkItem* work,
 #define MR_GRAM_PAIR 1
 #endif
 inline bool gram_pair_of(int k) { return MR_GRAM_PAIR && k > 112 && k <= 128; }
+// waves (one work item each) per block of the one-wave Gram kernels
+#ifndef MR_GRAM_WAVES
+#define MR_GRAM_WAVES 4
+#endif
+constexpr int GRAM_WAVES = MR_GRAM_WAVES;
 inline int64_t gram_blocks(int64_t n_work, int k) {
-  return gram_pair_of(k) ? n_work : (n_work + 3) / 4;
+  return gram_pair_of(k) ? n_work : (n_work + GRAM_WAVES - 1) / GRAM_WAVES;
 }
 int launch_cg_start_split(hipStream_t s, bool user_side, int k, const SplitItem* split,
                           int64_t n_split, GramDst direct, const CgStart& cs, double* parts,

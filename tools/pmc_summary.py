@@ -20,6 +20,8 @@ CLASSES = [
     ("gram_items", r"gram_kernel<\d+, false|gram_pair_kernel<false"),
     ("matvec_users", r"(cg_matvec_kernel|cg_onepass_kernel)<\d+, true"),
     ("matvec_items", r"(cg_matvec_kernel|cg_onepass_kernel)<\d+, false"),
+    ("resident_users", r"cg_resident_kernel<\d+, true"),
+    ("resident_items", r"cg_resident_kernel<\d+, false"),
     ("slab_reduce", r"slab_reduce_kernel"),
     ("cg_update", r"cg_update_kernel"),
     ("cg_control", r"cg_control_kernel"),
