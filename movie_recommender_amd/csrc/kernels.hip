@@ -1244,6 +1244,34 @@ __device__ __forceinline__ void gst(float* p, float v) {
   if (MR_G_NT) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
+// MR_G_WIDE: a tile leaves as ONE 16-byte store per lane (the whole 1 KiB
+// tile contiguous per wave instruction) instead of four 4-byte stores of
+// 4 x 64 B.  Lane (q, 4j + i) holds rows 4q .. 4q+3 of column 4j + i; a
+// quad-local 4 x 4 transpose (DPP quad_perm: lane ^ 2, then lane ^ 1) gives
+// it row 4q + i, columns 4j .. 4j+3.  Same bytes at the same addresses.
+#ifndef MR_G_WIDE
+#define MR_G_WIDE 0
+#endif
+template <int CTRL>
+__device__ __forceinline__ float dpp_quad(float s) {
+  return __builtin_bit_cast(float,
+                            __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, s), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ floatx4 quad_transpose(floatx4 v, int i) {
+  const bool hi = (i & 2) != 0, odd = (i & 1) != 0;
+  float r0 = dpp_quad<0x4E>(hi ? v[0] : v[2]);   // quad_perm [2,3,0,1]
+  float r1 = dpp_quad<0x4E>(hi ? v[1] : v[3]);
+  if (hi) { v[0] = r0; v[1] = r1; } else { v[2] = r0; v[3] = r1; }
+  r0 = dpp_quad<0xB1>(odd ? v[0] : v[1]);         // quad_perm [1,0,3,2]
+  r1 = dpp_quad<0xB1>(odd ? v[2] : v[3]);
+  if (odd) { v[0] = r0; v[2] = r1; } else { v[1] = r0; v[3] = r1; }
+  return v;
+}
+__device__ __forceinline__ void gst4(float* p, floatx4 v) {
+  if (MR_PROBE_GRAM == 1) return;
+  if (MR_G_NT) __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(p));
+  else *reinterpret_cast<floatx4*>(p) = v;
+}
 
 template <int NB, bool USER, bool FUSE, bool BUF>
 __device__ __forceinline__ void gram_wave(
@@ -1411,32 +1439,60 @@ __device__ __forceinline__ void gram_wave(
   // exec-mask branches per wave.)  Plain stores: 4-byte sc1 write-through
   // stores, to keep the gathered rows in L2, made the kernel 4 % slower.
   constexpr int NO = NB * (NB - 1) / 2, NF = NB / 2, NTILE = NO + NF + (NB & 1);
-  float* __restrict__ Gl = Gd + 64 * q + col;
+  if constexpr (MR_G_WIDE) {
+    float* __restrict__ Gw = Gd + 64 * q + 16 * (col & 3) + 4 * (col >> 2);
 #pragma unroll
-  for (int bi = 0; bi < NB; ++bi) {
+    for (int bi = 0; bi < NB; ++bi) {
 #pragma unroll
-    for (int bj = bi + 1; bj < NB; ++bj) {
-      const int t = acc_tile(bi, bj, NB), o = off_index(bi, bj, NB) * 256;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) gst(&Gl[o + 16 * r], acc[t][r]);
+      for (int bj = bi + 1; bj < NB; ++bj) {
+        const int t = acc_tile(bi, bj, NB), o = off_index(bi, bj, NB) * 256;
+        gst4(&Gw[o], quad_transpose(acc[t], col & 3));
+      }
     }
-  }
 #pragma unroll
-  for (int m = 0; m < NF; ++m) {
-    const int te = acc_tile(2 * m, 2 * m, NB), to = acc_tile(2 * m + 1, 2 * m + 1, NB);
-    float dg = 0.f;
+    for (int m = 0; m < NF; ++m) {
+      const int te = acc_tile(2 * m, 2 * m, NB), to = acc_tile(2 * m + 1, 2 * m + 1, NB);
+      float dg = 0.f;
+      floatx4 f;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = 4 * q + r;
-      gst(&Gl[(NO + m) * 256 + 16 * r], col >= row ? acc[te][r] : acc[to][r]);
-      if (col - 4 * q == r) dg = acc[to][r];
+      for (int r = 0; r < 4; ++r) {
+        const int row = 4 * q + r;
+        f[r] = col >= row ? acc[te][r] : acc[to][r];
+        if (col - 4 * q == r) dg = acc[to][r];
+      }
+      gst4(&Gw[(NO + m) * 256], quad_transpose(f, col & 3));
+      if ((col >> 2) == q) gst(&Gd[NTILE * 256 + m * 16 + col], dg);   // D_2m+1's diagonal
     }
-    if ((col >> 2) == q) gst(&Gd[NTILE * 256 + m * 16 + col], dg);   // D_2m+1's diagonal
-  }
-  if constexpr ((NB & 1) != 0) {
-    const int t = acc_tile(NB - 1, NB - 1, NB);
+    if constexpr ((NB & 1) != 0)
+      gst4(&Gw[(NO + NF) * 256], quad_transpose(acc[acc_tile(NB - 1, NB - 1, NB)], col & 3));
+  } else {
+    float* __restrict__ Gl = Gd + 64 * q + col;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) gst(&Gl[(NO + NF) * 256 + 16 * r], acc[t][r]);
+    for (int bi = 0; bi < NB; ++bi) {
+#pragma unroll
+      for (int bj = bi + 1; bj < NB; ++bj) {
+        const int t = acc_tile(bi, bj, NB), o = off_index(bi, bj, NB) * 256;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gst(&Gl[o + 16 * r], acc[t][r]);
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < NF; ++m) {
+      const int te = acc_tile(2 * m, 2 * m, NB), to = acc_tile(2 * m + 1, 2 * m + 1, NB);
+      float dg = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 4 * q + r;
+        gst(&Gl[(NO + m) * 256 + 16 * r], col >= row ? acc[te][r] : acc[to][r]);
+        if (col - 4 * q == r) dg = acc[to][r];
+      }
+      if ((col >> 2) == q) gst(&Gd[NTILE * 256 + m * 16 + col], dg);   // D_2m+1's diagonal
+    }
+    if constexpr ((NB & 1) != 0) {
+      const int t = acc_tile(NB - 1, NB - 1, NB);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) gst(&Gl[(NO + NF) * 256 + 16 * r], acc[t][r]);
+    }
   }
   if constexpr (FUSE) {
     if (!to_slab)
@@ -1836,6 +1892,7 @@ __device__ __forceinline__ void gram_pair_wave(
     D.Gn[di * D.sS] = (float)wlen;
   }
   float* __restrict__ Gl = Gd + 64 * q + col;
+  float* __restrict__ Gw = Gd + 64 * q + 16 * (col & 3) + 4 * (col >> 2);   // MR_G_WIDE
   auto store_tiles = [&](auto own) {
 #pragma unroll
     for (int bi = 0; bi < NB; ++bi) {
@@ -1843,20 +1900,27 @@ __device__ __forceinline__ void gram_pair_wave(
       for (int bj = bi + 1; bj < NB; ++bj) {
         if (pair_owner(bi, bj) != decltype(own)::value) continue;
         const int t = pair_local(bi, bj), o = off_index(bi, bj, NB) * 256;
+        if constexpr (MR_G_WIDE) {
+          gst4(&Gw[o], quad_transpose(acc[t], col & 3));
+        } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) gst(&Gl[o + 16 * r], acc[t][r]);
+          for (int r = 0; r < 4; ++r) gst(&Gl[o + 16 * r], acc[t][r]);
+        }
       }
     }
 #pragma unroll
     for (int m = 2 * decltype(own)::value; m < 2 * decltype(own)::value + 2; ++m) {
       const int te = pair_local(2 * m, 2 * m), to = pair_local(2 * m + 1, 2 * m + 1);
       float dg = 0.f;
+      floatx4 f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = 4 * q + r;
-        gst(&Gl[(NO + m) * 256 + 16 * r], col >= row ? acc[te][r] : acc[to][r]);
+        f[r] = col >= row ? acc[te][r] : acc[to][r];
+        if (!MR_G_WIDE) gst(&Gl[(NO + m) * 256 + 16 * r], f[r]);
         if (col - 4 * q == r) dg = acc[to][r];
       }
+      if (MR_G_WIDE) gst4(&Gw[(NO + m) * 256], quad_transpose(f, col & 3));
       if ((col >> 2) == q) gst(&Gd[NTILE * 256 + m * 16 + col], dg);   // D_2m+1's diagonal
     }
   };
@@ -2033,7 +2097,7 @@ static int launch_gram_nb(hipStream_t s, bool user_side, int k, const WorkItem* 
   constexpr bool BUFOK = NB % 4 == 0;
   const bool buf = BUFOK && (int64_t)(zrow + 1) * ldk_of(k) * 4 < ((int64_t)1 << 31);
 #define MR_GRAM_LAUNCH(U, FU, B, R)                                                          \
-  MR_LAUNCH((gram_kernel<NB, U, FU, B, R>), dim3((unsigned)grid), dim3(256), 0, s, work, n_work, \
+  MR_LAUNCH((gram_kernel<NB, U, FU, B, R>), dim3((unsigned)grid), dim3(64 * GRAM_WAVES), 0, s, work, n_work, \
             idx, val, F, bias, k, ldk_of(k), zrow, direct, slab, cs)
 #define MR_GRAM_USER(FU, B)                                                                 \
   if (rhs_mfma) MR_GRAM_LAUNCH(true, FU, B, true); else MR_GRAM_LAUNCH(true, FU, B, false);
