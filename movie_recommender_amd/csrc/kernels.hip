@@ -1031,7 +1031,9 @@ struct RowSrc {
   uint32_t colb;                  // BUF path: this lane's column offset, bytes
 };
 // Timing probes of the Gram's streams (wrong results; never in the product
-// build): MR_PROBE_GRAM 1 drops the G stores, 2 the row gathers (each row
+// build): MR_PROBE_GRAM 1 drops the G stores, 3 sends them all to the first
+// 8 entities' G (an L2-resident region: the same stores without their HBM
+// writes), 2 the row gathers (each row
 // replaced by a value derived from its id, so the id / weight stream stays)
 #ifndef MR_PROBE_GRAM
 #define MR_PROBE_GRAM 0
@@ -1241,7 +1243,7 @@ __device__ __forceinline__ void bf3_mfma(floatx4 (&acc)[NB * (NB + 1) / 2], floa
 #endif
 __device__ __forceinline__ void gst(float* p, float v) {
   if (MR_PROBE_GRAM == 1) return;
-  if (MR_G_NT) __builtin_nontemporal_store(v, p);
+  if (MR_G_NT && MR_PROBE_GRAM != 3) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
 // MR_G_WIDE: a tile leaves as ONE 16-byte store per lane (the whole 1 KiB
@@ -1269,7 +1271,7 @@ __device__ __forceinline__ floatx4 quad_transpose(floatx4 v, int i) {
 }
 __device__ __forceinline__ void gst4(float* p, floatx4 v) {
   if (MR_PROBE_GRAM == 1) return;
-  if (MR_G_NT) __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(p));
+  if (MR_G_NT && MR_PROBE_GRAM != 3) __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(p));
   else *reinterpret_cast<floatx4*>(p) = v;
 }
 
@@ -1411,7 +1413,7 @@ __device__ __forceinline__ void gram_wave(
   const bool to_slab = wslab >= 0;
   const int64_t di = to_slab ? (int64_t)wslab : (int64_t)went;
   const GramDst& D = to_slab ? slab : direct;
-  float* __restrict__ Gd = D.G + di * D.sG;
+  float* __restrict__ Gd = D.G + (MR_PROBE_GRAM == 3 ? (di & 7) : di) * D.sG;
   float* __restrict__ Cd = D.C + di * D.sV;
   if (q == 0) {
 #pragma unroll
@@ -1871,7 +1873,7 @@ __device__ __forceinline__ void gram_pair_wave(
   const bool to_slab = wslab >= 0;
   const int64_t di = to_slab ? (int64_t)wslab : (int64_t)went;
   const GramDst& D = to_slab ? slab : direct;
-  float* __restrict__ Gd = D.G + di * D.sG;
+  float* __restrict__ Gd = D.G + (MR_PROBE_GRAM == 3 ? (di & 7) : di) * D.sG;
   float* __restrict__ Cd = D.C + di * D.sV;
   if (q == 0) {
 #pragma unroll

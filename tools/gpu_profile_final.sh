@@ -10,7 +10,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 step() {  # name, seconds, command...
   local name=$1 secs=$2; shift 2
-  echo "[$TAG] $name"
+  echo "[$TAG] $name" >&2
   timeout -k 10 $secs "$@"
   local rc=$?
   if [ $rc -ne 0 ]; then echo "$name rc=$rc: stop"; exit $rc; fi
@@ -18,6 +18,7 @@ step() {  # name, seconds, command...
 step bench 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err
 tail -c 400 $OUT/bench.json
 step trace 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --no-cpu --steps 20 --warmup 5 > $OUT/bench_under_rocprof.json 2> $OUT/trace.err
+python tools/rocprof_agree.py $OUT/trace $OUT/bench_under_rocprof.json --out $OUT/rocprof_vs_events.json > /dev/null
 for K in 64 128; do
   # counters per CG iteration: the launch-per-iteration path (the resident
   # solve makes the same accesses per iteration, bench.py scales by its
