@@ -947,6 +947,12 @@ bool Engine::onepass_for(const Side& S) const {
   return onepass && k <= kMaxK && (!sharded() || peer_on);
 }
 
+// The user-side rhs / row sums on the matrix cores (the W block) from NB =
+// MR_RHSM_MIN_NB up (A/B knob; below it they stay on the VALU)
+#ifndef MR_RHSM_MIN_NB
+#define MR_RHSM_MIN_NB 5
+#endif
+
 // start: the Gram waves also start the CG solve (r0, p0, q0 = G p0 and the
 // block pairs of r.r / p.Gp); Engine::cg(started = true) finishes the start.
 int Engine::gram(Side& S, bool start) {
@@ -960,7 +966,7 @@ int Engine::gram(Side& S, bool start) {
   const CgStart cs = cg_start_of(S);
   if (launch_gram(stream, user, k, S.work, S.n_work, S.idx, S.val, F, bias, zrow,
                   direct_dst(S), slab_dst(S), start ? &cs : nullptr,
-                  user && rhs_mfma && w_bf16 && nb16_of(k) >= 5))
+                  user && rhs_mfma && w_bf16 && nb16_of(k) >= MR_RHSM_MIN_NB))
     return -1;
   if (toc(cls, -1, a)) return -1;
   if (S.n_split) {

@@ -75,3 +75,32 @@ def test_bench_gpus2_matches_gpus1(gpu):
     assert dc["model_step_ms"] == pytest.approx(m["compute_ms"] + m["exchange_ms"]
                                                 + m["peer_reductions_ms"], abs=1e-3)
     assert "decomposition" not in a
+
+
+@pytest.mark.gpu
+def test_bench_forced_shard_world1_resident_peer(gpu):
+    """One rank through the whole sharded path on its own GPU: RCCL
+    communicator, the peer all-reduce (mapped onto its own buffer) and the
+    resident CG solve together -- the combination an N-GPU run uses, which the
+    shared-GPU layouts above cannot run (they switch the resident solve off).
+    Same trajectory as the unsharded run, a decomposed line, and the peer
+    reductions counted."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+           "MASTER_PORT": str(port)}
+    one = run_bench(["--gpus", "1"] + SMALL)
+    assert one.returncode == 0, one.stderr[-3000:]
+    sh = run_bench(["--gpus", "1", "--force-shard"] + SMALL, env=env)
+    assert sh.returncode == 0, sh.stderr[-3000:]
+    a = json.loads([ln for ln in one.stdout.splitlines() if ln.strip()][0])
+    b = json.loads([ln for ln in sh.stdout.splitlines() if ln.strip()][0])
+    assert b["config"]["parallelism"] == "shard1"
+    assert b["config"]["cg_scalars"].startswith("peer"), b["config"]["cg_scalars"]
+    assert "resident_users" in b["kernels"] and "resident_items" in b["kernels"]
+    assert a["cg_iterations"] == b["cg_iterations"]
+    assert a["trajectory"]["cg_per_iteration"] == b["trajectory"]["cg_per_iteration"]
+    dc = b["decomposition"]
+    assert dc["peer_reductions_per_step"] >= 2 and dc["peer_wait_ms_per_step"] > 0
