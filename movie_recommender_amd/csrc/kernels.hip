@@ -1241,9 +1241,15 @@ __device__ __forceinline__ void bf3_mfma(floatx4 (&acc)[NB * (NB + 1) / 2], floa
 #ifndef MR_G_NT
 #define MR_G_NT 1
 #endif
+// MR_G_SC1 (A/B knob): the G stores write-through (`sc1`: the line leaves
+// L2 instead of staying there dirty)
+#ifndef MR_G_SC1
+#define MR_G_SC1 0
+#endif
 __device__ __forceinline__ void gst(float* p, float v) {
   if (MR_PROBE_GRAM == 1) return;
-  if (MR_G_NT && MR_PROBE_GRAM != 3) __builtin_nontemporal_store(v, p);
+  if (MR_G_SC1) asm volatile("global_store_dword %0, %1, off sc1" : : "v"(p), "v"(v) : "memory");
+  else if (MR_G_NT && MR_PROBE_GRAM != 3) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
 // MR_G_WIDE: a tile leaves as ONE 16-byte store per lane (the whole 1 KiB
@@ -1271,7 +1277,12 @@ __device__ __forceinline__ floatx4 quad_transpose(floatx4 v, int i) {
 }
 __device__ __forceinline__ void gst4(float* p, floatx4 v) {
   if (MR_PROBE_GRAM == 1) return;
-  if (MR_G_NT && MR_PROBE_GRAM != 3) __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(p));
+  // s_nop: a store of more than 8 bytes reads its data VGPRs after issue, so
+  // a VALU write to them needs wait states the hazard recognizer cannot see
+  // through an asm statement
+  if (MR_G_SC1)
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+  else if (MR_G_NT && MR_PROBE_GRAM != 3) __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(p));
   else *reinterpret_cast<floatx4*>(p) = v;
 }
 
