@@ -140,6 +140,14 @@ __device__ double xsum_value(const int64_t* c_in) {
   return ldexp(v, kXLsb);
 }
 
+// General-CG SpMV (csr_spmv_kernel) timing probes (wrong results; never in the product build), bit mask:
+// 1 no gathers, 2 no LDS staging / row sums (each thread sums its own
+// entries), 4 no output stores, 8 no row-offset loads; the CG then runs
+// to max_iteration (no stagnation or small-residual stop)
+#ifndef MR_SP_PROBE
+#define MR_SP_PROBE 0
+#endif
+
 // Block-level flush of each wave's per-lane containers of NV sums into the
 // global bins [kXBins][NV][kXW] (bin = block mod kXBins, agent-scope integer
 // atomics: exact, so their order does not matter).
@@ -2629,7 +2637,7 @@ __device__ __forceinline__ void apply_beta(CgScalars& v, double rr2) {
   v.final_rr = rr2;
   const double beta = rr2 / v.rr;
   v.beta = beta;
-  if (beta > 1.0 - v.min_dec) v.fails += 1;
+  if (!MR_SP_PROBE && beta > 1.0 - v.min_dec) v.fails += 1;
   else v.fails = 0;
   if (v.fails >= 2) {
     v.done = 1;
@@ -2637,7 +2645,7 @@ __device__ __forceinline__ void apply_beta(CgScalars& v, double rr2) {
   } else {
     v.rr = rr2;
     v.it += 1;
-    if (v.it >= v.max_it || rr2 < 1e-6) {
+    if (v.it >= v.max_it || (rr2 < 1e-6 && !MR_SP_PROBE)) {
       v.done = 1;
       v.ret = v.it;
     }
@@ -2843,7 +2851,7 @@ __device__ void cg_finalize(CgState* st, int phase, double s, CgMirror* mirror, 
     v.fails = 0;
     v.done = 0;
     v.ret = 0;
-    if (v.max_it <= 0 || s < 1e-6) v.done = 1;
+    if (v.max_it <= 0 || (s < 1e-6 && !MR_SP_PROBE)) v.done = 1;
     store_state(st, v);
     publish(v, mirror, seq);
   } else if (phase == CG_ALPHA) {
@@ -4259,7 +4267,7 @@ __device__ void start_rule(CgState* st, CgMirror* mirror, int seq, double min_de
     v.ret = 0;
     v.comm0 = rr;
     v.comm1 = pq;
-    v.done = (max_it <= 0 || rr < 1e-6) ? 1 : 0;
+    v.done = (max_it <= 0 || (rr < 1e-6 && !MR_SP_PROBE)) ? 1 : 0;
     if (!v.done) {
       v.alpha = rr / pq;
       v.comm0 = pq;      // sharded updates derive alpha as rr / comm[0]
@@ -4587,6 +4595,12 @@ int launch_predict(hipStream_t s, int64_t n, int k, int ldk, const int* uid,
 // r + alpha*q, sum += v*x.
 // ---------------------------------------------------------------------------
 constexpr int SP_THREADS = 256;
+#ifndef MR_SP_ORDER   // 1: a block's gathers issued before the next block's stream loads
+#define MR_SP_ORDER 1
+#endif
+#ifndef MR_SP_OUT   // policy of the output stores: 0 default, 1 non-temporal, 2 write-through (sc1)
+#define MR_SP_OUT 0
+#endif
 #ifndef MR_SP_AUX   // cache policy of the once-read id / value streams (0: default; nt measured 4 % slower)
 #define MR_SP_AUX 0
 #endif
@@ -4628,8 +4642,12 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
         return xa[GATHER == SPG_P0 ? 2 * (int64_t)c + 1 : (int64_t)c];
     }
   };
+  double probe_sink = 0.0;
   auto emit = [&](int64_t row, double s) {
-    out[row] = s;
+    if (MR_SP_PROBE & 4) probe_sink += s;
+    else if (MR_SP_OUT == 1) __builtin_nontemporal_store(s, out + row);
+    else if (MR_SP_OUT == 2) asm volatile("global_store_dwordx2 %0, %1, off sc1" : : "v"(out + row), "v"(s) : "memory");
+    else out[row] = s;
     if constexpr (OUT == SPO_CG) {   // pv = the interleaved (r, p) pairs
       double pn = pv[2 * row + 1];
       if (update_p) {
@@ -4651,7 +4669,7 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
   struct Stage {
     int32_t cc[PER];
     double vv[PER];
-    int32_t rpo;
+    int64_t ro;   // rp[first row + t] (raw: converted where it is used)
   };
   auto load_short = [&](Stage& S, int64_t r0, int64_t r1, int64_t n0, int64_t n1) {
     if constexpr (BUF) {
@@ -4693,7 +4711,15 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
         S.cc[u] = j < n1 ? c : 0;
       }
     }
-    S.rpo = (t < r1 - r0) ? (int32_t)(rp[r0 + t] - n0) : 0;
+    // every thread loads (a clamped row: rp holds rows + 1 entries) and the
+    // offset is formed where it is used: a load under `t < rows` (or a select
+    // right behind it) made the compiler wait for it at once -- draining the
+    // next block's stream loads issued just before
+    const int64_t nr = r1 - r0;
+    if (MR_SP_PROBE & 8)
+      S.ro = n0 + min((int64_t)t * ((n1 - n0) / (nr > 0 ? nr : 1)), n1 - n0);
+    else
+      S.ro = rp[r0 + (t < nr ? t : nr)];
   };
   Stage cur, nxt;
   int64_t b = blockIdx.x;
@@ -4716,6 +4742,15 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
   for (; b < n_blk; b += gs) {
     const bool has_next = b + gs < n_blk, has_next2 = b + 2 * gs < n_blk;
     const bool next_short = has_next && qn1 - qn0 <= SP_TILE;
+    const bool cur_short = n1 - n0 <= SP_TILE;
+    double gx[PER];
+    if (MR_SP_ORDER && cur_short) {
+      // this block's gathers first, then the next block's stream: waiting for
+      // the gathers (in-order vmcnt) then leaves the stream in flight
+#pragma unroll
+      for (int u = 0; u < PER; ++u) gx[u] = (MR_SP_PROBE & 1) ? 1.0 + (double)cur.cc[u] : gather(cur.cc[u]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     if (next_short) load_short(nxt, qr0, qr1, qn0, qn1);
     int64_t sr0 = 0, sr1 = 0, sn0 = 0, sn1 = 0;   // bounds of block b + 2 gs
     if (has_next2) {
@@ -4724,19 +4759,34 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
       sr1 = blk[2 * (b + 2 * gs) + 2];
       sn1 = blk[2 * (b + 2 * gs) + 3];
     }
-    if (n1 - n0 <= SP_TILE) {
-      double gx[PER];
+    if (cur_short) {
+      if (!MR_SP_ORDER) {
 #pragma unroll
-      for (int u = 0; u < PER; ++u) gx[u] = gather(cur.cc[u]);
+        for (int u = 0; u < PER; ++u) gx[u] = (MR_SP_PROBE & 1) ? 1.0 + (double)cur.cc[u] : gather(cur.cc[u]);
+      }
       const int nl = (int)(n1 - n0);
+      if constexpr ((MR_SP_PROBE & 2) != 0) {
+        double sum = 0.0;
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+          const int jl = BUF ? 2 * (256 * (u >> 1) + t) + (u & 1) : t + u * SP_THREADS;
+          if (jl < nl) sum += cur.vv[u] * gx[u];
+        }
+        const int R = (int)(r1 - r0);
+        if (t < R) emit(r0 + t, sum + (double)cur.ro);
+      } else {
 #pragma unroll
       for (int u = 0; u < PER; ++u) {
         const int jl = BUF ? 2 * (256 * (u >> 1) + t) + (u & 1)
                            : t + u * SP_THREADS;   // load_short's entry map
-        if (jl < nl) prod[jl] = cur.vv[u] * gx[u];
+        // unconditional (jl < SP_TILE always; products past the block are
+        // never read): a store under `jl < nl` put the wait for its gather
+        // inside a branch, where the wait-count pass falls back to vmcnt(0)
+        // -- draining the next block's stream loads
+        if (MR_SP_ORDER || jl < nl) prod[jl] = cur.vv[u] * gx[u];
       }
       const int R = (int)(r1 - r0);
-      if (t < R) srp[t] = cur.rpo;
+      if (t < R) srp[t] = (int32_t)(cur.ro - n0);
       if (t == 0) srp[R] = (int32_t)(n1 - n0);
       __syncthreads();
       int G = 1;
@@ -4761,6 +4811,7 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
       for (int o = G / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
       if (lr < R && g == 0) emit(r0 + lr, sum);
       __syncthreads();   // prod / srp are reused by the next block
+      }
     } else {             // one long row: per-thread strided sums, fixed-order tree
       double sum = 0.0;
       for (int64_t j = n0 + t; j < n1; j += SP_THREADS) sum += v[j] * gather(ci[j]);
@@ -4771,6 +4822,9 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
     r0 = qr0; r1 = qr1; n0 = qn0; n1 = qn1;
     qr0 = sr0; qr1 = sr1; qn0 = sn0; qn1 = sn1;
     cur = nxt;
+  }
+  if constexpr ((MR_SP_PROBE & 4) != 0) {
+    if (probe_sink == 1.2345e300) out[blockIdx.x] = probe_sink;   // keeps the work alive
   }
   if constexpr (OUT == SPO_CG) {
     const double tot = block_sum_f64<SP_THREADS>(d, sh);
