@@ -78,6 +78,7 @@ __device__ T block_sum_t(T v, T* sh) {
 // broadcasts; candidate rows are staged 16 factors at a time.
 // ---------------------------------------------------------------------------
 constexpr int SC_U = 32, SC_C = 256, SC_KC = 16;
+typedef uint32_t sc_u32x2 __attribute__((ext_vector_type(2)));
 
 template <bool KEYS>
 __global__ __launch_bounds__(256) void rec_score_kernel(
@@ -158,24 +159,46 @@ __global__ __launch_bounds__(256) void rec_score_kernel(
     }
     __syncthreads();
   }
+  // Epilogue, branch-free but for the wave-uniform user test: the 8 users'
+  // biases and the 4 candidates' medians are loaded together (clamped
+  // indices) before any use, and each user's row goes out through a buffer
+  // resource ending at n_cand, so a candidate past the end is a store the
+  // hardware drops, not a branch.  With per-(user, candidate) range tests the
+  // wait-count pass put a vmcnt(0) at every store's block -- each one waited
+  // for the previous stores and atomics to complete, 32 serialized memory
+  // round trips per thread.
+  double medv[4], biasv[8];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = c0 + tx + 64 * q;
+    medv[q] = med[c < n_cand ? c : n_cand - 1];
+  }
 #pragma unroll
   for (int p = 0; p < 8; ++p) {
-    const int u = u0 + ty * 8 + p;   // wave-uniform
+    const int u = u0 + ty * 8 + p;
+    biasv[p] = X[(int64_t)(u < n_users ? u : n_users - 1) * (k + 1) + k];
+  }
+  const int nrow = n_cand - c0;   // candidates of this tile in range (> 0)
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int u = __builtin_amdgcn_readfirstlane(u0 + ty * 8 + p);   // wave-uniform
     if (u >= n_users) continue;
-    const double bias = X[(int64_t)u * (k + 1) + k];
+    const __amdgpu_buffer_rsrc_t row = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<char*>(out) + ((int64_t)u * ld + c0) * 8, (short)0,
+        (int)(min(nrow, SC_C) * 8), 0x00020000);
     unsigned long long lo = ~0ull, hi = 0ull;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int c = c0 + tx + 64 * q;
-      if (c >= n_cand) continue;
-      const double s = add_rn(add_rn(acc[p][q], bias), med[c]);
+      const int cl = tx + 64 * q;   // candidate c0 + cl
+      const double s = add_rn(add_rn(acc[p][q], biasv[p]), medv[q]);
       if constexpr (KEYS) {
         const uint64_t key = score_key(s);
-        reinterpret_cast<uint64_t*>(out)[(int64_t)u * ld + c] = key;
-        lo = min(lo, (unsigned long long)key);
-        hi = max(hi, (unsigned long long)key);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(sc_u32x2, key), row, cl * 8, 0, 0);
+        const bool ok = cl < nrow;
+        lo = min(lo, ok ? (unsigned long long)key : ~0ull);
+        hi = max(hi, ok ? (unsigned long long)key : 0ull);
       } else {
-        reinterpret_cast<double*>(out)[(int64_t)u * ld + c] = s;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(sc_u32x2, s), row, cl * 8, 0, 0);
       }
     }
     if constexpr (KEYS) {   // per-user key range: the select skips the common prefix
