@@ -4598,6 +4598,9 @@ constexpr int SP_THREADS = 256;
 #ifndef MR_SP_ORDER   // 1: a block's gathers issued before the next block's stream loads
 #define MR_SP_ORDER 1
 #endif
+#ifndef MR_SP_PRELOAD   // 1: the CG output pass preloads its rows' (r, p) pairs
+#define MR_SP_PRELOAD 1
+#endif
 #ifndef MR_SP_OUT   // policy of the output stores: 0 default, 1 non-temporal, 2 write-through (sc1)
 #define MR_SP_OUT 0
 #endif
@@ -4657,6 +4660,19 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
       d += pn * s;
     }
   };
+  // the CG output pass with the row's (r, p) pair loaded beside the block's
+  // gathers (and staged in LDS for the summing thread) instead of after the
+  // row sum: the same arithmetic without a dependent global load per block
+  auto emit_cg = [&](int64_t row, double s, double2 rp) {
+    if (MR_SP_PROBE & 4) probe_sink += s;
+    else out[row] = s;
+    double pn = rp.y;
+    if (update_p) {
+      pn = -1.0 * rp.x + beta * pn;   // vect_add(-1, r, beta, p, p)
+      pv[2 * row + 1] = pn;
+    }
+    d += pn * s;
+  };
   // Software pipeline over the workgroup's row blocks b, b + grid, ...: the
   // next short block's column ids, values and row offsets are loaded into a
   // second register set at the top of the current block (in flight during
@@ -4666,6 +4682,7 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
   // row sums are unchanged: results are bitwise those of the plain loop.
   constexpr int PER = SP_TILE / SP_THREADS;
   __shared__ int32_t srp[kSpMaxRows + 1];   // the block's row offsets - n0
+  __shared__ double2 spv[OUT == SPO_CG && MR_SP_PRELOAD && MR_SP_ORDER ? kSpMaxRows : 1];   // their (r, p) pairs
   struct Stage {
     int32_t cc[PER];
     double vv[PER];
@@ -4720,6 +4737,7 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
       S.ro = n0 + min((int64_t)t * ((n1 - n0) / (nr > 0 ? nr : 1)), n1 - n0);
     else
       S.ro = rp[r0 + (t < nr ? t : nr)];
+
   };
   Stage cur, nxt;
   int64_t b = blockIdx.x;
@@ -4744,11 +4762,16 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
     const bool next_short = has_next && qn1 - qn0 <= SP_TILE;
     const bool cur_short = n1 - n0 <= SP_TILE;
     double gx[PER];
+    double2 rpair;   // OUT == SPO_CG: row r0 + t's (r, p) pair, loaded with the gathers
     if (MR_SP_ORDER && cur_short) {
       // this block's gathers first, then the next block's stream: waiting for
       // the gathers (in-order vmcnt) then leaves the stream in flight
 #pragma unroll
       for (int u = 0; u < PER; ++u) gx[u] = (MR_SP_PROBE & 1) ? 1.0 + (double)cur.cc[u] : gather(cur.cc[u]);
+      if constexpr (OUT == SPO_CG && MR_SP_PRELOAD) {
+        const int64_t nr = r1 - r0;
+        rpair = reinterpret_cast<const double2*>(pv)[r0 + (t < nr ? t : nr - 1)];
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
     if (next_short) load_short(nxt, qr0, qr1, qn0, qn1);
@@ -4788,6 +4811,9 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
       const int R = (int)(r1 - r0);
       if (t < R) srp[t] = (int32_t)(cur.ro - n0);
       if (t == 0) srp[R] = (int32_t)(n1 - n0);
+      if constexpr (OUT == SPO_CG && MR_SP_PRELOAD && MR_SP_ORDER) {
+        if (t < R) spv[t] = rpair;
+      }
       __syncthreads();
       int G = 1;
       while (G < 64 && 2 * G * R <= SP_THREADS) G *= 2;
@@ -4809,7 +4835,10 @@ __global__ __launch_bounds__(SP_THREADS) void csr_spmv_kernel(
         }
       }
       for (int o = G / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
-      if (lr < R && g == 0) emit(r0 + lr, sum);
+      if (lr < R && g == 0) {
+        if constexpr (OUT == SPO_CG && MR_SP_PRELOAD && MR_SP_ORDER) emit_cg(r0 + lr, sum, spv[lr]);
+        else emit(r0 + lr, sum);
+      }
       __syncthreads();   // prod / srp are reused by the next block
       }
     } else {             // one long row: per-thread strided sums, fixed-order tree
