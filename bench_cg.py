@@ -40,6 +40,21 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0
+# per-launch HBM bytes from rocprofv3 PMC passes of this bench
+# (tools/probes/r06pmc_cg.sh -> profiles/r06/pmc_cg.json)
+PMC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r06", "pmc_cg.json")
+PMC_KERNEL = {"spmv_a": "void mr::csr_spmv_kernel<1, 0, true>",
+              "spmv_at": "void mr::csr_spmv_kernel<0, 1, true>",
+              "update": "mr::cgls_update_kernel"}
+
+
+def pmc_traffic(cls, rows, cols, per_row):
+    """HBM bytes per launch of kernel class `cls` from the committed PMC
+    summary -- only for the shape it was collected on (the default one)."""
+    if (rows, cols, per_row) != (27_000_000, 2_800_000, 10) or not os.path.exists(PMC_FILE):
+        return None
+    ent = json.load(open(PMC_FILE)).get("per_kernel", {}).get(PMC_KERNEL.get(cls, ""))
+    return ent["bytes_corrected"] if ent else None
 PUBLISHED = {"ms_per_cg_iteration": {
     "c5.18xlarge alg1 (SpMV^T) 4/9/18/36/72 threads": [763, 422, 275, 360, 367],
     "c5.18xlarge alg2 (explicit transpose) 4/9/18/36/72 threads": [1042, 481, 261, 278, 208],
@@ -154,7 +169,8 @@ def main():
         "roofline": {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                      "alg_bytes_per_launch": table[dom]["alg_bytes"],
-                     "avg_launch_us": table[dom]["avg_us"], "traffic": None},
+                     "avg_launch_us": table[dom]["avg_us"],
+                     "traffic": pmc_traffic(dom, rows, cols, k)},
         "iteration_roofline": {"alg_bytes_per_cg_iteration": per_it_bytes,
                                "GBps": round(per_it_bytes / (ms_it / 1e3) / 1e9, 1),
                                "frac": round(per_it_bytes / (ms_it / 1e3) / 1e9 / HBM_PEAK_GBS, 4)},
