@@ -244,6 +244,10 @@ __global__ __launch_bounds__(256) void rec_exclude_kernel(uint64_t* __restrict__
 // MovieLens-like scores that is one histogram pass and one collect pass.
 // ---------------------------------------------------------------------------
 constexpr int SEL_NT = 512, SEL_CAP = 2048, SEL_D = 11, SEL_BINS = 1 << SEL_D;
+#ifndef MR_SEL_U
+#define MR_SEL_U 4
+#endif
+constexpr int SEL_U = MR_SEL_U;   // keys in flight per thread in the passes over a user's row
 typedef unsigned __int128 u128;
 
 __device__ __forceinline__ u128 composite(uint64_t key, uint32_t mid) {
@@ -275,7 +279,19 @@ __global__ __launch_bounds__(SEL_NT) void rec_select_kernel(
   if (lin) {
     for (int i = tid; i < SEL_BINS; i += SEL_NT) hist[i] = 0;
     __syncthreads();
-    for (int c = tid; c < n_cand; c += SEL_NT) {
+    // SEL_U keys per thread in flight before any is used (one load, one
+    // wait and one LDS atomic per trip left a block one 512-thread row of
+    // keys in flight); counts are order-free, so the result is unchanged
+    int c = tid;
+    for (; c + (SEL_U - 1) * SEL_NT < n_cand; c += SEL_U * SEL_NT) {
+      uint64_t kk[SEL_U];
+#pragma unroll
+      for (int j = 0; j < SEL_U; ++j) kk[j] = K[c + j * SEL_NT];
+#pragma unroll
+      for (int j = 0; j < SEL_U; ++j)
+        if (kk[j] != 0) atomicAdd(&hist[bin_of(kk[j])], 1u);
+    }
+    for (; c < n_cand; c += SEL_NT) {
       const uint64_t key = K[c];
       if (key != 0) atomicAdd(&hist[bin_of(key)], 1u);
     }
@@ -339,10 +355,10 @@ __global__ __launch_bounds__(SEL_NT) void rec_select_kernel(
   // collect every element with composite >= P
   if (tid == 0) s_n = 0;
   __syncthreads();
-  for (int c = tid; c < n_cand; c += SEL_NT) {
-    const uint64_t key = K[c];
-    if (key == 0) continue;
-    const uint32_t m = (uint32_t)mid[c];
+  // (SEL_U keys and ids in flight per thread, as in the histogram; the slot
+  // order depends on the atomics' order, the sort below fixes the result)
+  auto take = [&](uint64_t key, uint32_t m) {
+    if (key == 0) return;
     if (lin_b >= 0 ? bin_of(key) >= lin_b : composite(key, m) >= P) {
       const int slot = atomicAdd(&s_n, 1);
       if (slot < SEL_CAP) {
@@ -350,6 +366,21 @@ __global__ __launch_bounds__(SEL_NT) void rec_select_kernel(
         cm[slot] = m;
       }
     }
+  };
+  {
+    int c = tid;
+    for (; c + (SEL_U - 1) * SEL_NT < n_cand; c += SEL_U * SEL_NT) {
+      uint64_t kk[SEL_U];
+      uint32_t mm[SEL_U];
+#pragma unroll
+      for (int j = 0; j < SEL_U; ++j) {
+        kk[j] = K[c + j * SEL_NT];
+        mm[j] = (uint32_t)mid[c + j * SEL_NT];
+      }
+#pragma unroll
+      for (int j = 0; j < SEL_U; ++j) take(kk[j], mm[j]);
+    }
+    for (; c < n_cand; c += SEL_NT) take(K[c], (uint32_t)mid[c]);
   }
   __syncthreads();
   const int n = min(s_n, SEL_CAP);

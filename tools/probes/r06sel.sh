@@ -1,0 +1,14 @@
+# Top-N select: SEL_U keys in flight per thread in its passes over a user's
+# row (base: 4) against 1 (round 5's loop) and 8; serving tests first
+set -o pipefail
+OUT=gpurun_out/r06sel; mkdir -p $OUT; export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_serving.py -m gpu > $OUT/tests.log 2>&1 || { echo "tests rc=$?"; tail -20 $OUT/tests.log; exit 1; }
+tail -1 $OUT/tests.log
+for v in base sel1 sel8 base sel1 sel8; do
+  if [ $v = base ]; then unset MR_LIB_PATH; else export MR_LIB_PATH=$PWD/var_libs/$v/cpp_ls_lib.so; fi
+  timeout -k 10 300 python -u bench_serving.py --what topn --no-cpu > $OUT/topn_$v.json 2> $OUT/topn_$v.err || { echo "bench $v rc=$?"; tail -3 $OUT/topn_$v.err; exit 1; }
+  python3 -c "
+import json
+for ln in open('$OUT/topn_$v.json'):
+    d=json.loads(ln); r=d.get('roofline',{}); print('$v', round(d.get('value')), d.get('unit'), 'score_ms', r.get('avg_launch_ms'), 'select_ms', r.get('select_ms'), 'select_GBps', r.get('select_GBps_2pass'))"
+done
