@@ -32,6 +32,10 @@ namespace mr {
 constexpr int SM_RS = 4096;    // movies per accumulation range
 constexpr int SM_CAP = 2048;   // candidate list capacity (LDS)
 constexpr int SM_NT = 1024;    // threads per query workgroup
+#ifndef MR_SM_U
+#define MR_SM_U 4
+#endif
+constexpr int SM_U = MR_SM_U;   // (movie, rating) entries per thread in flight
 
 static unsigned sgrid(int64_t n) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 16384));
@@ -209,19 +213,45 @@ __global__ __launch_bounds__(SM_NT) void sim_find_kernel(
         __syncthreads();
         const int total = s_tot;
         const int nu = (int)min<int64_t>(SM_NT, moff[i + 1] - t0);
-        for (int e = tid; e < total; e += SM_NT) {
+        // SM_U entries per thread: their (movie, rating) loads all issued
+        // before the first is used (one load pair, one wait and two LDS
+        // atomics per trip kept one entry per thread in flight); integer
+        // atomics, so the order does not matter
+        auto locate = [&](int e, int& p, unsigned& rk) {
           int a = 0, b = nu;   // last rater k with s_pre[k] <= e
           while (b - a > 1) {
             const int mid = (a + b) >> 1;
             if (s_pre[mid] <= e) a = mid;
             else b = mid;
           }
-          const int p = s_lo[a] + (e - s_pre[a]);
-          const unsigned rk = s_ri[a];
-          const int jj = umov[p] - base;
-          const unsigned rj = ur2[p];
+          p = s_lo[a] + (e - s_pre[a]);
+          rk = s_ri[a];
+        };
+        auto add = [&](int jj, unsigned rk, unsigned rj) {
           atomicAdd(&accA[jj], ((unsigned long long)(rk * rj) << 32) | 1ull);
           atomicAdd(&accB[jj], ((unsigned long long)(rk * rk) << 32) | (unsigned long long)(rj * rj));
+        };
+        int e = tid;
+        for (; e + (SM_U - 1) * SM_NT < total; e += SM_U * SM_NT) {
+          int pp[SM_U];
+          unsigned rkk[SM_U];
+#pragma unroll
+          for (int j = 0; j < SM_U; ++j) locate(e + j * SM_NT, pp[j], rkk[j]);
+          int jv[SM_U];
+          unsigned rjv[SM_U];
+#pragma unroll
+          for (int j = 0; j < SM_U; ++j) {
+            jv[j] = umov[pp[j]];
+            rjv[j] = ur2[pp[j]];
+          }
+#pragma unroll
+          for (int j = 0; j < SM_U; ++j) add(jv[j] - base, rkk[j], rjv[j]);
+        }
+        for (; e < total; e += SM_NT) {
+          int p;
+          unsigned rk;
+          locate(e, p, rk);
+          add(umov[p] - base, rk, ur2[p]);
         }
         __syncthreads();
       }
