@@ -229,8 +229,18 @@ __global__ __launch_bounds__(256) void rec_exclude_kernel(uint64_t* __restrict__
                                                           const int64_t* __restrict__ off,
                                                           const int* __restrict__ cand) {
   const int u = blockIdx.x;
-  for (int64_t i = off[u] + threadIdx.x; i < off[u + 1]; i += blockDim.x)
-    keys[(int64_t)u * ld + cand[i]] = 0;
+  // 4 candidate ids loaded before the stores: with a store pending every
+  // load wait is a full drain, so one id per trip serialized the stores
+  const int64_t e = off[u + 1];
+  int64_t i = off[u] + threadIdx.x;
+  for (; i + 3 * (int64_t)blockDim.x < e; i += 4 * (int64_t)blockDim.x) {
+    int c[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c[j] = cand[i + j * (int64_t)blockDim.x];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) keys[(int64_t)u * ld + c[j]] = 0;
+  }
+  for (; i < e; i += blockDim.x) keys[(int64_t)u * ld + cand[i]] = 0;
 }
 
 // ---------------------------------------------------------------------------
